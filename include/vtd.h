@@ -1,0 +1,202 @@
+/*
+ * vtd.h — C-ABI of libvtd.so, the MI355X (gfx950) forward path of the Vision
+ * Transformer detector of westlake-moonlight/vision_transformer_detector.
+ *
+ * The reference has no FFI: its forward is a Keras graph whose arithmetic runs in
+ * TensorFlow 2.9.1's own kernels.  Each entry point below replaces one layer class
+ * of that graph (cited as vtd.py:N = /root/reference/vision_transformer_detector.py);
+ * `vtd_forward` replaces the whole `model(images, training=False)` call.
+ *
+ * Conventions
+ *  - Every pointer argument named *_dev is DEVICE memory owned by the caller.  The
+ *    library never allocates or frees memory inside a compute call and keeps no
+ *    pointer after it returns.  `stream` is a hipStream_t (NULL = default stream).
+ *  - Calls are asynchronous on `stream`, perform no host synchronisation and no
+ *    allocation, and are therefore HIP-graph capturable.
+ *  - Return value: VTD_OK (0) or a negative vtd_status; `vtd_last_error()` returns a
+ *    thread-local message for the last failure on the calling thread.
+ *  - "Padded" widths: every activation/weight row is padded with zeros to a multiple
+ *    of VTD_KALIGN elements (see vtd_dims); pad columns are guaranteed zero on output.
+ */
+#ifndef VTD_H_
+#define VTD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VTD_ABI_VERSION 1
+#define VTD_KALIGN 64          /* K / row padding granule, elements              */
+#define VTD_MAX_MLP 16         /* max encoder_mlp_quantities                     */
+#define VTD_MAX_HEAD 64        /* max mlp_head layers * repeats                   */
+#define VTD_MAX_DETECT 17      /* Constants.MAX_DETECT_OBJECTS_QUANTITY vtd.py:28 */
+
+typedef enum vtd_status {
+  VTD_OK = 0,
+  VTD_ERR_INVALID_ARG = -1,    /* bad shape / null pointer / unsupported combo  */
+  VTD_ERR_UNSUPPORTED = -2,    /* dtype or size not supported by this build     */
+  VTD_ERR_HIP = -3,            /* a HIP runtime call failed (message has code)  */
+  VTD_ERR_WORKSPACE = -4       /* workspace too small                           */
+} vtd_status;
+
+typedef enum vtd_dtype {       /* compute (GEMM operand) dtype                   */
+  VTD_F32 = 0,                 /* parity mode: f32 operands, f32 MFMA            */
+  VTD_BF16 = 1                 /* throughput mode: bf16 operands, f32 accumulate */
+} vtd_dtype;
+
+typedef enum vtd_act {         /* activation fused in a GEMM epilogue            */
+  VTD_ACT_NONE = 0,
+  VTD_ACT_GELU_TANH = 1,       /* tfa.layers.GELU() approximate=True vtd.py:402 */
+  VTD_ACT_MISH = 2             /* MishActivation vtd.py:119-129                  */
+} vtd_act;
+
+/* create_vision_transformer_detector(...) kwargs, vtd.py:498-506.  dropout must be
+ * None/0 (inference), max_weight/clip_weight only act on training (no-ops here). */
+typedef struct vtd_config {
+  int batch;
+  int image_h, image_w, channels;     /* input_shape                              */
+  int patch_size;
+  int embedding_dim;
+  int num_heads;                      /* encoder_num_heads                        */
+  int key_dim;                        /* encoder_key_dim                          */
+  int mlp_quantities;                 /* encoder_mlp_quantities                   */
+  int repeat_times;                   /* encoder_repeat_times                     */
+  int head_last_units;                /* mlp_head_last_units                      */
+  int head_layers;                    /* mlp_head_dense_layers_quantity           */
+  int head_repeats;                   /* mlp_head_dense_mish_block_repeats        */
+  int use_mish;                       /* 1 = Mish, 0 = GELU(tanh)                 */
+  int dtype;                          /* vtd_dtype                                */
+} vtd_config;
+
+/* Derived sizes (elements).  Fill with vtd_derive_dims. */
+typedef struct vtd_dims {
+  int grid_h, grid_w;                 /* ceil(H/p), ceil(W/p)  (SAME padding)     */
+  int tokens;                         /* N = grid_h*grid_w                        */
+  int pad_top, pad_left;              /* SAME pad_before                          */
+  int patch_dim, patch_dim_p;         /* P = p*p*C and padded                     */
+  int d, d_p;                         /* embedding_dim and padded                 */
+  int key_dim_p;                      /* per-head padded key dim (32/64/128)      */
+  int inner_p;                        /* num_heads * key_dim_p                    */
+  int qkv_p;                          /* padded 3*inner_p                         */
+  int mlp_units[VTD_MAX_MLP];         /* encoder MLP widths                       */
+  int mlp_units_p[VTD_MAX_MLP];
+  int n_head;                         /* head Dense layers (excl. dense & final)  */
+  int head_units[VTD_MAX_HEAD];
+  int head_units_p[VTD_MAX_HEAD];
+  int tokens_p;                       /* head input width (Reshape) padded        */
+  int64_t rows;                       /* batch * tokens                           */
+  int64_t head_rows;                  /* batch * 17                               */
+} vtd_dims;
+
+/* Device pointers of one encoder block, packed by vtd_pack_dense / vtd_pack_vector.
+ * Matrices: dtype = cfg.dtype, layout W^T [N_p][K_p] (row = output unit).
+ * Vectors: fp32, padded with zeros. */
+typedef struct vtd_layer_weights {
+  const float* ln1_gamma; const float* ln1_beta;        /* [d_p]                  */
+  const void* w_qkv; const float* b_qkv;                /* [qkv_p][d_p], [qkv_p]  */
+  const void* w_out; const float* b_out;                /* [d_p][inner_p], [d_p]  */
+  const float* ln2_gamma; const float* ln2_beta;        /* [d_p]                  */
+  const void* w_mlp[VTD_MAX_MLP]; const float* b_mlp[VTD_MAX_MLP];
+} vtd_layer_weights;
+
+typedef struct vtd_weights {
+  const void* w_patch; const float* b_patch;            /* [d_p][patch_dim_p]     */
+  const float* pos_embedding;                           /* [tokens] fp32          */
+  const vtd_layer_weights* layers;                      /* HOST array [repeat_times] */
+  const void* w_det; const float* b_det;                /* Dense(17): [64][d_p]   */
+  const void* w_head[VTD_MAX_HEAD]; const float* b_head[VTD_MAX_HEAD];
+  const void* w_final; const float* b_final;            /* Dense(6): [64][136_p]  */
+} vtd_weights;
+
+/* ---------------------------------------------------------------- library ------ */
+int vtd_abi_version(void);
+const char* vtd_last_error(void);
+
+/* Shapes of the graph built by create_vision_transformer_detector (vtd.py:498-583). */
+int vtd_derive_dims(const vtd_config* cfg, vtd_dims* out);
+
+/* Bytes of scratch `vtd_forward` needs for this config (256-B aligned buffers). */
+int vtd_workspace_bytes(const vtd_config* cfg, size_t* bytes);
+
+/* ---------------------------------------------------------------- weights ------ */
+/* Pack a Keras Dense/EinsumDense kernel (fp32, row-major [K][N], device) into the
+ * transposed, zero-padded compute layout dst[n_row_offset + n'][k'] (dtype), where
+ * k' = (k / k_group) * k_group_p + k % k_group   (per-head K padding, attention_output)
+ * n' = (n / n_group) * n_group_p + n % n_group   (per-head N padding, query/key/value).
+ * Pass k_group = k_group_p = K (resp. N) for no grouping.  dst must be pre-zeroed. */
+int vtd_pack_dense(const float* src_dev, int K, int N, int k_group, int k_group_p,
+                   int n_group, int n_group_p, void* dst_dev, int ld_dst,
+                   int n_row_offset, int dtype, void* stream);
+/* Same re-indexing for a bias / LN vector (fp32 -> fp32). */
+int vtd_pack_vector(const float* src_dev, int N, int n_group, int n_group_p,
+                    float* dst_dev, int offset, void* stream);
+
+/* ---------------------------------------------------------------- per-op ------- */
+/* ExtractImagePatches (vtd.py:177-206) + Reshape flatten_patches (vtd.py:279-280):
+ * images NHWC fp32 [B][H][W][C] -> patches [B*N][ld_out] (dtype), SAME zero pad,
+ * (kh, kw, c) order; columns [P, ld_out) written as zero. */
+int vtd_extract_patches(const float* images_dev, int B, int H, int W, int C, int p,
+                        void* out_dev, int ld_out, int dtype, void* stream);
+
+/* Dense + activation (vtd.py:297, 389-403, 454, 472-483, 489):
+ * C[m][n] = act(sum_k A[m][k] * Bt[n][k] + bias[n] + rowadd[m % rowadd_period]
+ *               (rowadd only for n < rowadd_ncols)) + resid[m][n]
+ * for m < M, n < N.  A, Bt in `dtype`; K % VTD_KALIGN == 0; lda, ldb % 8 == 0.
+ * out: fp32 (out_dtype 0) or bf16 (1); out2 (nullable) a second bf16 copy.
+ * scatter_tokens > 0 selects the head Reshape epilogue (vtd.py:461-463): element
+ * (m = b*T + t, n < 17) is stored at out[(b*17 + f / T) * ldo + f % T], f = t*17 + n. */
+typedef struct vtd_epilogue {
+  const float* bias;            /* [N] or NULL                                    */
+  const float* rowadd;          /* position embedding per row, or NULL            */
+  int rowadd_period, rowadd_ncols;
+  int act;                      /* vtd_act                                         */
+  const float* resid; int ldr;  /* fp32 residual (may alias out), or NULL          */
+  void* out; int ldo; int out_dtype;
+  void* out2; int ldo2;         /* optional bf16 copy                              */
+  int scatter_tokens;
+} vtd_epilogue;
+int vtd_gemm(int M, int N, int K, const void* A_dev, int lda, const void* Bt_dev,
+             int ldb, int dtype, const vtd_epilogue* epi, void* stream);
+
+/* keras LayerNormalization(axis=-1, epsilon) (vtd.py:353-357, 375-379):
+ * x fp32 [rows][ldx] -> y (dtype) [rows][ldy]; stats over the first D columns;
+ * columns [D, ldy) of y written as zero. */
+int vtd_layernorm(const float* x_dev, int64_t rows, int D, int ldx,
+                  const float* gamma_dev, const float* beta_dev, float eps,
+                  void* y_dev, int ldy, int dtype, void* stream);
+
+/* keras MultiHeadAttention core (vtd.py:364-369): per batch b, head h,
+ * O = softmax(scale * Q K^T) V with Q, K, V read from qkv [B*N][ldqkv] at column
+ * offsets h*dkp, inner + h*dkp, 2*inner + h*dkp (inner = heads*dkp); O written to
+ * out [B*N][ldo] at column h*dkp.  dkp in {32, 64, 128}; scale = 1/sqrt(key_dim). */
+int vtd_attention(const void* qkv_dev, int B, int N, int heads, int dkp, int ldqkv,
+                  float scale, void* out_dev, int ldo, int dtype, void* stream);
+
+/* transform_predictions (vtd.py:586-647): logits fp32 [n][6] -> detections fp32
+ * [sigmoid, sigmoid*79, clip(sigmoid)*608 x4]. */
+int vtd_decode(const float* logits_dev, int64_t n, float* dets_dev, void* stream);
+
+/* ---------------------------------------------------------------- forward ------ */
+/* model(images, training=False) (vtd.py:579-581, ipynb:836):
+ * images NHWC fp32 [B][H][W][C] in [-1, 1] -> logits fp32 [B][17][6] (pre-sigmoid),
+ * and, if dets_dev != NULL, transform_predictions(logits) fp32 [B][17][6]. */
+int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images_dev,
+                float* logits_dev, float* dets_dev, void* workspace_dev,
+                size_t workspace_bytes, void* stream);
+
+/* Optional per-kernel timing of vtd_forward (hipEvents on `stream`, recorded around
+ * every launch while enabled).  vtd_profile_read returns per-class totals in ms
+ * summed over the forwards since the last reset; classes: 0 gemm, 1 attention,
+ * 2 layernorm, 3 patches, 4 other. Also returns per-class launch counts and FLOPs. */
+#define VTD_PROF_CLASSES 5
+int vtd_profile_enable(int enable);
+int vtd_profile_reset(void);
+int vtd_profile_read(double* ms, int64_t* launches, double* flops, int n_classes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VTD_H_ */

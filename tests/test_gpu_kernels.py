@@ -1,0 +1,262 @@
+"""Per-kernel parity on the GPU, through the C-ABI (include/vtd.h).
+
+Each HIP kernel is compared with the fp64 oracle op it replaces (oracle/vtd_numpy.py)
+or a plain fp64 torch restatement of the same op, on seeded inputs.  bf16 operands are
+rounded to bf16 BEFORE the reference runs, so GEMM checks measure accumulation error
+only.  Tolerances are written per test.
+"""
+import ctypes
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import vtd_numpy as ref
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def L(cuda):
+    from vision_transformer_detector_amd import _lib
+    return _lib
+
+
+def _dt(L, name):
+    return {"f32": (L.F32, torch.float32), "bf16": (L.BF16, torch.bfloat16)}[name]
+
+
+def _gemm(L, A, Bt, dtype, N=None, bias=None, rowadd=None, rowadd_period=1,
+          rowadd_ncols=0, act=0, resid=None, out=None, out_dtype=0, out2=None,
+          scatter_tokens=0, ldo=None):
+    M, K = A.shape
+    N = N if N is not None else Bt.shape[0]
+    e = L.VtdEpilogue()
+    e.bias = L.ptr(bias)
+    e.rowadd = L.ptr(rowadd)
+    e.rowadd_period, e.rowadd_ncols = rowadd_period, rowadd_ncols
+    e.act = act
+    e.resid = L.ptr(resid)
+    e.ldr = resid.shape[1] if resid is not None else 0
+    e.out = L.ptr(out)
+    e.ldo = ldo if ldo is not None else out.shape[-1]
+    e.out_dtype = out_dtype
+    e.out2 = L.ptr(out2)
+    e.ldo2 = out2.shape[1] if out2 is not None else 0
+    e.scatter_tokens = scatter_tokens
+    L.check(L.lib.vtd_gemm(M, N, K, A.data_ptr(), A.shape[1], Bt.data_ptr(), Bt.shape[1],
+                           dtype, ctypes.byref(e), L.stream_ptr()), "vtd_gemm")
+    torch.cuda.synchronize()
+
+
+def _np_act(act, x):
+    return {0: lambda v: v, 1: ref.gelu_tanh, 2: ref.mish}[act](x)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 200, 192), (1, 17, 64),
+                                   (515, 770, 128), (64, 6, 256)])
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_gemm_bias_act(L, cuda, dtype, M, N, K, act):
+    code, tdt = _dt(L, dtype)
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K + act)
+    A = torch.randn(M, K, generator=g).to(tdt)
+    Bt = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(tdt)
+    bias = torch.randn(N, generator=g)
+    ref64 = A.double() @ Bt.double().T + bias.double()
+    ref64 = torch.from_numpy(_np_act(act, ref64.numpy()))
+    out = torch.full((M, N), float("nan"), device=cuda)
+    _gemm(L, A.to(cuda), Bt.to(cuda), code, bias=bias.to(cuda), act=act, out=out)
+    err = (out.cpu().double() - ref64).abs().max().item()
+    # f32: exact fp32 fma chain, <= ~1e-6 relative to the row norms; bf16 inputs are
+    # exact in fp32, so only accumulation order differs.
+    assert err <= 2e-5 * max(1.0, ref64.abs().max().item()), err
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_gemm_epilogue_rowadd_resid_out2(L, cuda, dtype):
+    code, tdt = _dt(L, dtype)
+    M, N, K, T = 392, 192, 128, 196
+    g = torch.Generator().manual_seed(5)
+    A = torch.randn(M, K, generator=g).to(tdt)
+    Bt = (torch.randn(N, K, generator=g) / 12).to(tdt)
+    bias = torch.randn(N, generator=g)
+    pos = torch.randn(T, generator=g)
+    resid = torch.randn(M, N, generator=g)
+    ncols = 150
+    ref64 = A.double() @ Bt.double().T + bias.double()
+    rows = torch.arange(M) % T
+    ref64[:, :ncols] += pos.double()[rows][:, None]
+    ref64 = torch.from_numpy(ref.mish(ref64.numpy())) + resid.double()
+    out = resid.clone().to(cuda)              # in-place residual like the encoder
+    out2 = torch.zeros(M, N, dtype=torch.bfloat16, device=cuda)
+    _gemm(L, A.to(cuda), Bt.to(cuda), code, bias=bias.to(cuda), rowadd=pos.to(cuda),
+          rowadd_period=T, rowadd_ncols=ncols, act=2, resid=out, out=out, out2=out2)
+    assert (out.cpu().double() - ref64).abs().max().item() < 1e-4
+    assert torch.equal(out2.cpu(), out.cpu().to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_gemm_bf16_output(L, cuda, dtype):
+    code, tdt = _dt(L, dtype)
+    M, N, K = 256, 384, 64
+    g = torch.Generator().manual_seed(9)
+    A = torch.randn(M, K, generator=g).to(tdt)
+    Bt = torch.randn(N, K, generator=g).to(tdt)
+    out = torch.zeros(M, N, dtype=torch.bfloat16, device=cuda)
+    _gemm(L, A.to(cuda), Bt.to(cuda), code, out=out, out_dtype=1)
+    ref64 = A.double() @ Bt.double().T
+    rel = ((out.cpu().double() - ref64).abs() / ref64.abs().clamp_min(1e-3)).max().item()
+    assert rel < 8e-3     # one bf16 rounding of the output (2^-8)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("T", [196, 37, 1])
+def test_gemm_head_reshape_scatter(L, cuda, dtype, T):
+    """Dense(17) + keras Reshape((17, -1)) (vtd.py:454-463) as a scatter epilogue:
+    must equal the row-major reinterpretation, NOT a transpose."""
+    code, tdt = _dt(L, dtype)
+    B, K = 3, 64
+    g = torch.Generator().manual_seed(T)
+    A = torch.randn(B * T, K, generator=g).to(tdt)
+    Bt = torch.randn(17, K, generator=g).to(tdt)
+    bias = torch.randn(17, generator=g)
+    ld = ((T + 63) // 64) * 64
+    out = torch.full((B * 17, ld), 7.0, device=cuda)
+    out[:, T:] = 0
+    _gemm(L, A.to(cuda), Bt.to(cuda), code, bias=bias.to(cuda), out=out, N=17,
+          scatter_tokens=T, ldo=ld)
+    t = (A.double() @ Bt.double().T + bias.double()).reshape(B, T, 17)
+    u = t.reshape(B, 17, T)                     # row-major reshape
+    got = out.cpu().double()[:, :T].reshape(B, 17, T)
+    assert (got - u).abs().max().item() < 1e-4
+    assert (out.cpu()[:, T:] == 0).all()
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("D,ld", [(768, 768), (28, 64), (30, 64), (1024, 1024), (4100, 4160)])
+def test_layernorm(L, cuda, dtype, D, ld):
+    code, tdt = _dt(L, dtype)
+    rows = 37
+    g = torch.Generator().manual_seed(D)
+    x = torch.zeros(rows, ld)
+    x[:, :D] = torch.randn(rows, D, generator=g) * 3 + 1
+    gamma = torch.zeros(ld); gamma[:D] = 1 + 0.1 * torch.randn(D, generator=g)
+    beta = torch.zeros(ld); beta[:D] = 0.1 * torch.randn(D, generator=g)
+    y = torch.full((rows, ld), float("nan"), dtype=tdt, device=cuda)
+    L.check(L.lib.vtd_layernorm(x.to(cuda).data_ptr(), rows, D, ld, gamma.to(cuda).data_ptr(),
+                                beta.to(cuda).data_ptr(), 1e-3, y.data_ptr(), ld, code,
+                                L.stream_ptr()), "ln")
+    torch.cuda.synchronize()
+    exp = ref.layer_norm(x[:, :D].double().numpy(), gamma[:D].double().numpy(),
+                         beta[:D].double().numpy())
+    got = y.cpu().double().numpy()
+    tol = 1e-5 if dtype == "f32" else 1.6e-2
+    assert np.abs(got[:, :D] - exp).max() < tol * max(1, np.abs(exp).max())
+    assert (got[:, D:] == 0).all()
+
+
+def test_layernorm_epsilon_kat(L, cuda):
+    """variance 1e-3 must be scaled by 1/sqrt(2e-3)."""
+    D = 64
+    x = torch.tensor([(-1) ** i * math.sqrt(1e-3) for i in range(D)], dtype=torch.float32)
+    y = torch.zeros(1, D, device=cuda)
+    one, zero = torch.ones(D, device=cuda), torch.zeros(D, device=cuda)
+    L.check(L.lib.vtd_layernorm(x.to(cuda).data_ptr(), 1, D, D, one.data_ptr(),
+                                zero.data_ptr(), 1e-3, y.data_ptr(), D, L.F32, L.stream_ptr()))
+    torch.cuda.synchronize()
+    assert abs(y[0, 0].item() - math.sqrt(1e-3) / math.sqrt(2e-3)) < 1e-5
+
+
+def _attn_ref(qkv, B, N, H, dk, dkp):
+    q = qkv[:, :H * dkp].reshape(B, N, H, dkp)[..., :dk]
+    k = qkv[:, H * dkp:2 * H * dkp].reshape(B, N, H, dkp)[..., :dk]
+    v = qkv[:, 2 * H * dkp:3 * H * dkp].reshape(B, N, H, dkp)[..., :dk]
+    s = np.einsum("bqhd,bkhd->bhqk", q, k) / math.sqrt(dk)
+    p = ref.softmax(s, axis=-1)
+    return np.einsum("bhqk,bkhd->bqhd", p, v)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("B,N,H,dk", [(2, 196, 3, 64), (1, 70, 2, 40), (1, 1, 1, 32),
+                                      (1, 333, 2, 128), (1, 1296, 1, 40), (1, 64, 4, 20)])
+def test_attention(L, cuda, dtype, B, N, H, dk):
+    code, tdt = _dt(L, dtype)
+    dkp = 32 if dk <= 32 else (64 if dk <= 64 else 128)
+    ld = 3 * H * dkp + 8
+    g = np.random.default_rng(N * 10 + dk)
+    qkv = np.zeros((B * N, ld), np.float32)
+    for part in range(3):
+        for h in range(H):
+            c0 = part * H * dkp + h * dkp
+            qkv[:, c0:c0 + dk] = g.normal(0, 1.5, size=(B * N, dk))
+    qkv_t = torch.from_numpy(qkv).to(tdt)
+    ldo = H * dkp
+    out = torch.full((B * N, ldo), float("nan"), dtype=tdt, device=cuda)
+    L.check(L.lib.vtd_attention(qkv_t.to(cuda).data_ptr(), B, N, H, dkp, ld,
+                                1.0 / math.sqrt(dk), out.data_ptr(), ldo, code,
+                                L.stream_ptr()), "attention")
+    torch.cuda.synchronize()
+    exp = _attn_ref(qkv_t.double().numpy(), B, N, H, dk, dkp)
+    got = out.cpu().double().numpy().reshape(B, N, H, dkp)
+    # f32: exact-f32 MFMA + fp32 softmax; bf16: P rounded to bf16 before P.V
+    tol = 2e-5 if dtype == "f32" else 2e-2
+    assert np.abs(got[..., :dk] - exp).max() < tol * max(1.0, np.abs(exp).max())
+    assert (got[..., dk:] == 0).all()
+
+
+def test_attention_uniform_kat(L, cuda):
+    """with Q = 0 the softmax is uniform -> O = mean over keys of V."""
+    B, N, H, dkp = 1, 100, 2, 64
+    g = torch.Generator().manual_seed(1)
+    qkv = torch.zeros(B * N, 3 * H * dkp)
+    qkv[:, H * dkp:] = torch.randn(B * N, 2 * H * dkp, generator=g)
+    out = torch.zeros(B * N, H * dkp, device=cuda)
+    L.check(L.lib.vtd_attention(qkv.to(cuda).data_ptr(), B, N, H, dkp, 3 * H * dkp, 0.125,
+                                out.data_ptr(), H * dkp, L.F32, L.stream_ptr()))
+    torch.cuda.synchronize()
+    v = qkv[:, 2 * H * dkp:].double()
+    assert (out.cpu().double() - v.mean(0, keepdim=True)).abs().max() < 1e-5
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("H,W,p", [(5, 5, 2), (608, 608, 17), (224, 224, 16), (40, 36, 8),
+                                   (13, 7, 4)])
+def test_extract_patches(L, cuda, dtype, H, W, p):
+    code, tdt = _dt(L, dtype)
+    B, C = 2, 3
+    img = ref.synthetic_images(B, (H, W, C), seed=H + W)
+    exp = ref.extract_patches_same(img, p)
+    P = p * p * C
+    ld = ((P + 63) // 64) * 64
+    out = torch.full((B * exp.shape[1], ld), float("nan"), dtype=tdt, device=cuda)
+    L.check(L.lib.vtd_extract_patches(torch.from_numpy(img).to(cuda).data_ptr(), B, H, W, C,
+                                      p, out.data_ptr(), ld, code, L.stream_ptr()))
+    torch.cuda.synchronize()
+    got = out.cpu()
+    exp_t = torch.from_numpy(exp.reshape(-1, P)).to(tdt)
+    assert torch.equal(got[:, :P], exp_t)            # pure data movement: bit-exact
+    assert (got[:, P:] == 0).all()
+
+
+def test_decode_matches_oracle(L, cuda):
+    g = np.random.default_rng(3)
+    logits = g.normal(0, 4, size=(5, 17, 6)).astype(np.float32)
+    logits[0, 0] = 0.0
+    dets = torch.zeros(5, 17, 6, device=cuda)
+    L.check(L.lib.vtd_decode(torch.from_numpy(logits).to(cuda).data_ptr(), 5 * 17,
+                             dets.data_ptr(), L.stream_ptr()))
+    torch.cuda.synchronize()
+    exp = ref.transform_predictions(logits)
+    assert np.abs(dets.cpu().numpy() - exp).max() < 1e-3
+    # a zero logit decodes to [0.5, 39.5, 304, 304, 304, 304]
+    np.testing.assert_allclose(dets[0, 0].cpu().numpy(), [0.5, 39.5, 304, 304, 304, 304],
+                               rtol=1e-6)
+
+
+def test_bad_args_raise_value_error(L, cuda):
+    e = L.VtdEpilogue()
+    with pytest.raises(ValueError):
+        L.check(L.lib.vtd_gemm(16, 16, 30, 1, 32, 1, 32, L.BF16, ctypes.byref(e),
+                               L.stream_ptr()), "gemm")

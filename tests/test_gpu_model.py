@@ -1,0 +1,134 @@
+"""Whole-forward parity on the GPU: `Model(images)` (libvtd.so vtd_forward) against the
+fp64 oracle golden vectors (tests/golden/, made by make_golden.py).
+
+Tolerances:
+  float32 mode: |y - ref| <= 1e-3 |ref| + 1e-3 max|ref|   (north_star's 1e-3 rel-tol)
+  bfloat16 mode: |y - ref| <= 3e-2 |ref| + 3e-2 max|ref|  (bf16 operands, fp32 accumulate)
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import vtd_numpy as V
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+TOL = {"float32": 1e-3, "bfloat16": 3e-2}
+
+
+def within(y, ref, tol):
+    y, ref = np.asarray(y, np.float64), np.asarray(ref, np.float64)
+    bound = tol * np.abs(ref) + tol * np.abs(ref).max()
+    return bool(np.all(np.abs(y - ref) <= bound)), float(np.abs(y - ref).max() / np.abs(ref).max())
+
+
+def load_tiny(name):
+    z = np.load(os.path.join(GOLD, f"{name}.npz"))
+    kw = json.loads(str(z["kwargs"]))
+    if "input_shape" in kw:
+        kw["input_shape"] = tuple(kw["input_shape"])
+    w = {k[2:]: z[k] for k in z.files if k.startswith("w:")}
+    return kw, w, z["images"], z["logits"], z["dets"]
+
+
+@pytest.fixture(scope="module")
+def vtd(cuda):
+    import vision_transformer_detector_amd as m
+    return m
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("name", ["tiny_mish", "tiny_gelu", "tiny_seq400"])
+def test_tiny_golden(vtd, cuda, name, dtype):
+    kw, w, x, logits, dets = load_tiny(name)
+    model = vtd.create_vision_transformer_detector(**kw, dtype=dtype)
+    model.set_weights(w)
+    y, d = model.detect(torch.from_numpy(x).to(cuda))
+    ok, rel = within(y.cpu().numpy(), logits, TOL[dtype])
+    assert ok, f"{name} {dtype}: max rel err {rel:.3e}"
+    if dtype == "float32":
+        assert np.abs(d.cpu().numpy() - dets).max() < 1e-3 * 608
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("case", ["c1_default_b1", "c2_vitb16_b1"])
+def test_seeded_full_config(vtd, cuda, case, dtype):
+    spec = json.load(open(os.path.join(GOLD, "seeded_forward.json")))[case]
+    kw = dict(spec["kwargs"])
+    if "input_shape" in kw:
+        kw["input_shape"] = tuple(kw["input_shape"])
+    w = V.init_weights(seed=spec["weight_seed"], perturb=spec["perturb"], **kw)
+    shape = V.resolve_kwargs(**kw)["input_shape"]
+    x = V.synthetic_images(spec["batch"], shape, seed=spec["image_seed"],
+                           letterbox=spec["letterbox"])
+    model = vtd.create_vision_transformer_detector(**kw, dtype=dtype)
+    model.set_weights(w)
+    y = model(torch.from_numpy(x).to(cuda), training=False).cpu().numpy()
+    ok, rel = within(y, np.array(spec["logits"]), TOL[dtype])
+    assert ok, f"{case} {dtype}: max rel err {rel:.3e}"
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_batch_rows_independent(vtd, cuda, dtype):
+    """Images never interact (no batch statistics): forward(batch)[i] == forward(img i).
+    This is the property the data-parallel sharding relies on."""
+    kw, w, x, _, _ = load_tiny("tiny_mish")
+    model = vtd.create_vision_transformer_detector(**kw, dtype=dtype)
+    model.set_weights(w)
+    xb = torch.from_numpy(x).to(cuda)
+    full = model(xb)
+    for i in range(x.shape[0]):
+        one = model(xb[i:i + 1])
+        assert torch.equal(one[0], full[i])
+
+
+def test_predict_and_decode_api(vtd, cuda):
+    kw, w, x, logits, dets = load_tiny("tiny_gelu")
+    model = vtd.create_vision_transformer_detector(**kw, dtype="float32")
+    model.set_weights(w)
+    y = model.predict(x, batch_size=1)
+    assert isinstance(y, np.ndarray) and y.shape == logits.shape and y.dtype == np.float32
+    ok, _ = within(y, logits, 1e-3)
+    assert ok
+    d = vtd.transform_predictions(torch.from_numpy(y).to(cuda)).cpu().numpy()
+    assert np.abs(d - V.transform_predictions(y)).max() < 1e-3
+    # get_weights round-trips in Keras order
+    names = model.weight_names()
+    assert names == list(V.weight_shapes(**kw))
+    got = model.get_weights()
+    for n, a in zip(names, got):
+        np.testing.assert_array_equal(a, w[n])
+
+
+def test_input_shape_mismatch_raises(vtd, cuda):
+    model = vtd.create_vision_transformer_detector(
+        input_shape=(32, 32, 3), patch_size=8, embedding_dim=16, encoder_num_heads=2,
+        encoder_key_dim=8, encoder_mlp_quantities=2, encoder_repeat_times=1,
+        mlp_head_last_units=8, mlp_head_dense_layers_quantity=2, dtype="float32")
+    with pytest.raises(ValueError):
+        model(torch.zeros(1, 33, 32, 3, device=cuda))
+    out = model(torch.zeros(2, 32, 32, 3, device=cuda))
+    assert out.shape == (2, 17, 6) and torch.isfinite(out).all()
+
+
+def test_hip_graph_capture_replays_forward(vtd, cuda):
+    """vtd_forward does no sync/alloc: it can be captured in a HIP graph and replayed."""
+    kw, w, x, logits, _ = load_tiny("tiny_seq400")
+    model = vtd.create_vision_transformer_detector(**kw, dtype="float32")
+    model.set_weights(w)
+    xb = torch.from_numpy(x).to(cuda)
+    eager = model(xb).clone()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        model(xb)                      # allocate workspace outside capture
+        g = torch.cuda.CUDAGraph()
+        logits_buf = torch.empty(x.shape[0], 17, 6, device=cuda)
+        with torch.cuda.graph(g, stream=s):
+            out = model.forward(xb)
+            logits_buf.copy_(out)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(logits_buf, eager)

@@ -1,0 +1,14 @@
+"""MI355X-native forward path of westlake-moonlight/vision_transformer_detector.
+
+Drop-in for the reference's `model(images, training=False)` / `model.predict` path
+(`vision_transformer_detector.py:498-647`): the same `create_vision_transformer_detector`
+kwargs, NHWC fp32 images in, (B, 17, 6) logits out, `transform_predictions` decode.
+All arithmetic runs in hand-written gfx950 HIP kernels in `libvtd.so` (C-ABI:
+`include/vtd.h`); importing this package fails if that library is missing.
+"""
+from .detector import (Constants, Model, create_vision_transformer_detector,  # noqa: F401
+                       keras_default_init, keras_weight_names, transform_predictions)
+from . import presets  # noqa: F401
+
+__all__ = ["Constants", "Model", "create_vision_transformer_detector",
+           "transform_predictions", "presets"]

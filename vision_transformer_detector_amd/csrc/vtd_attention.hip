@@ -1,0 +1,276 @@
+// keras MultiHeadAttention core (vtd.py:364-369; [upstream] key = value = x, scores
+// scaled by 1/sqrt(key_dim), softmax over keys) as a flash-style kernel: scores never
+// leave registers.
+//
+// One workgroup = NW waves = 32*NW queries of one (image b, head h); K and V are
+// streamed through LDS in tiles of 64 keys, shared by all waves of the workgroup.
+// Per wave, per 32-key block, the scores are computed SWAPPED: S^T = K . Q^T with the
+// 32x32 MFMA, so lane l owns query (l & 31) and 16 of the block's keys in registers:
+// the row max is 15 in-register fmax + one exchange with lane l ^ 32, and the row sum
+// needs no exchange until the end.  The exponentiated tile P^T is then directly the B
+// operand of O^T += V^T . P^T (the accumulator's rows are the keys being summed), so
+// P never touches LDS; V is staged transposed (Vt[d][key]) so the A operand is two
+// 8-byte LDS reads per MFMA.
+//   bf16: v_mfma_f32_32x32x16_bf16 (8 elements per lane per operand)
+//   f32 : v_mfma_f32_32x32x2_f32  (1 element per lane per operand)
+// Generic lane map used by both (E = elements per lane): lane half h = l >> 5 supplies
+// k = 2E*step + h*E + j; accumulator register rho holds row (rho&3) + 8(rho>>2) + 4h.
+#include <type_traits>
+
+#include "vtd_common.h"
+
+namespace vtd {
+
+namespace {
+
+constexpr int KVT = 64;   // keys per LDS tile
+
+template <typename T, int DKP>
+struct AttnCfg {
+  static constexpr int E = sizeof(T) == 2 ? 8 : 1;          // elements per lane
+  static constexpr int KSTEPS = DKP / (2 * E);              // MFMA k-steps over d
+  static constexpr int KROW = DKP * (int)sizeof(T) + (sizeof(T) == 2 ? 16 : 4);
+  static constexpr int VROW = KVT * (int)sizeof(T) + (sizeof(T) == 2 ? 8 : 4);
+  static constexpr int LDS = KVT * KROW + DKP * VROW;
+  static constexpr int DB = DKP / 32;                       // 32-wide d blocks
+};
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+template <typename T, int DKP>
+__global__ __launch_bounds__(512) void attention_kernel(
+    const T* __restrict__ qkv, int N, int heads, int ldqkv, float scale_log2,
+    T* __restrict__ out, int ldo) {
+  using C = AttnCfg<T, DKP>;
+  using OpT = typename std::conditional<sizeof(T) == 2, bf16x8, float>::type;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* k_lds = smem;
+  char* v_lds = smem + KVT * C::KROW;
+
+  const int tid = threadIdx.x, nthreads = blockDim.x;
+  const int lane = tid & 63, wave = tid >> 6, half = lane >> 5, col = lane & 31;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int inner = heads * DKP;
+  const int64_t row0 = (int64_t)b * N;
+  const int q0 = (blockIdx.x * (nthreads >> 6) + wave) * 32;
+  const bool active = q0 < N;
+
+  // ---- Q fragment of this lane's query, kept in registers for the whole kernel
+  OpT qf[C::KSTEPS];
+  {
+    const int q = min(q0 + col, N - 1);
+    const T* qp = qkv + (row0 + q) * ldqkv + h * DKP;
+#pragma unroll
+    for (int s = 0; s < C::KSTEPS; ++s) {
+      if constexpr (sizeof(T) == 2)
+        qf[s] = *reinterpret_cast<const bf16x8*>(qp + s * 16 + half * 8);
+      else
+        qf[s] = qp[s * 2 + half];
+    }
+  }
+
+  f32x16 o[C::DB];
+#pragma unroll
+  for (int i = 0; i < C::DB; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+
+  const int chunks_per_row = DKP * (int)sizeof(T) / 16;   // 16-B chunks per K/V row
+  for (int kv0 = 0; kv0 < N; kv0 += KVT) {
+    __syncthreads();   // previous tile fully consumed
+    // ---- stage K tile [key][d] and V^T tile [d][key]
+    for (int c = tid; c < KVT * chunks_per_row; c += nthreads) {
+      const int kr = c / chunks_per_row, ch = c - kr * chunks_per_row;
+      const int key = min(kv0 + kr, N - 1);
+      const T* base = qkv + (row0 + key) * ldqkv + h * DKP + ch * (16 / (int)sizeof(T));
+      const i32x4 kv = *reinterpret_cast<const i32x4*>(base + inner);
+      const i32x4 vv = *reinterpret_cast<const i32x4*>(base + 2 * inner);
+      if constexpr (sizeof(T) == 2) {
+        *reinterpret_cast<i32x4*>(k_lds + kr * C::KROW + ch * 16) = kv;
+        const bf16_t* ve = reinterpret_cast<const bf16_t*>(&vv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          *reinterpret_cast<bf16_t*>(v_lds + (ch * 8 + i) * C::VROW + kr * 2) = ve[i];
+      } else {
+        const float* ke = reinterpret_cast<const float*>(&kv);
+        const float* ve = reinterpret_cast<const float*>(&vv);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          *reinterpret_cast<float*>(k_lds + kr * C::KROW + (ch * 4 + i) * 4) = ke[i];
+          *reinterpret_cast<float*>(v_lds + (ch * 4 + i) * C::VROW + kr * 4) = ve[i];
+        }
+      }
+    }
+    __syncthreads();
+    if (!active) continue;
+
+    // ---- S^T = K . Q^T for the two 32-key blocks of the tile
+    f32x16 s[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+      const char* krow = k_lds + (kb * 32 + col) * C::KROW;
+#pragma unroll
+      for (int st = 0; st < C::KSTEPS; ++st) {
+        OpT a;
+        if constexpr (sizeof(T) == 2)
+          a = *reinterpret_cast<const bf16x8*>(krow + (st * 16 + half * 8) * 2);
+        else
+          a = *reinterpret_cast<const float*>(krow + (st * 2 + half) * 4);
+        s[kb] = mfma32(a, qf[st], s[kb]);
+      }
+    }
+    // ---- online softmax (base 2; scale folded into scale_log2)
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kv0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        float v = s[kb][r] * scale_log2;
+        v = key < N ? v : -INFINITY;
+        s[kb][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f(m_run - m_new);
+    m_run = m_new;
+    float psum = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = exp2f(s[kb][r] - m_new);
+        s[kb][r] = p;
+        psum += p;
+      }
+    l_run = l_run * alpha + psum;
+#pragma unroll
+    for (int i = 0; i < C::DB; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+
+    // ---- O^T += V^T . P^T
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      if constexpr (sizeof(T) == 2) {
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          bf16x8 pb;
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            pb[j] = static_cast<short>(f32_to_bf16(s[kb][8 * st + j]));
+          const int key_lo = kb * 32 + 16 * st + 4 * half;   // j = 0..3
+#pragma unroll
+          for (int db = 0; db < C::DB; ++db) {
+            const char* vr = v_lds + (db * 32 + col) * C::VROW;
+            const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vr + key_lo * 2);
+            const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vr + (key_lo + 8) * 2);
+            bf16x8 a;
+            a[0] = lo[0]; a[1] = lo[1]; a[2] = lo[2]; a[3] = lo[3];
+            a[4] = hi[0]; a[5] = hi[1]; a[6] = hi[2]; a[7] = hi[3];
+            o[db] = mfma32(a, pb, o[db]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          const int key = kb * 32 + (t & 3) + 8 * (t >> 2) + 4 * half;
+#pragma unroll
+          for (int db = 0; db < C::DB; ++db) {
+            const float a =
+                *reinterpret_cast<const float*>(v_lds + (db * 32 + col) * C::VROW + key * 4);
+            o[db] = mfma32(a, s[kb][t], o[db]);
+          }
+        }
+      }
+    }
+  }
+  if (!active) return;
+
+  // ---- normalise and store: lane owns query q0 + col, register rho -> d
+  const float l_tot = l_run + __shfl_xor(l_run, 32);
+  const float inv = 1.f / l_tot;
+  const int q = q0 + col;
+  if (q >= N) return;
+  T* op = out + (row0 + q) * ldo + h * DKP;
+#pragma unroll
+  for (int db = 0; db < C::DB; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = db * 32 + 8 * g + 4 * half;
+      if constexpr (sizeof(T) == 2) {
+        bf16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = static_cast<short>(f32_to_bf16(o[db][4 * g + r] * inv));
+        *reinterpret_cast<bf16x4*>(op + d) = v;
+      } else {
+        f32x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = o[db][4 * g + r] * inv;
+        *reinterpret_cast<f32x4*>(op + d) = v;
+      }
+    }
+}
+
+template <typename T, int DKP>
+int launch(const void* qkv, int B, int N, int heads, int ldqkv, float scale, void* out,
+           int ldo, hipStream_t stream) {
+  using C = AttnCfg<T, DKP>;
+  const int nq = (N + 31) / 32;
+  const int nw = nq <= 8 ? nq : 8;
+  dim3 grid((nq + nw - 1) / nw, heads, B);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_kernel<T, DKP>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr_set = true;
+  }
+  const float scale_log2 = scale * 1.4426950408889634f;
+  hipLaunchKernelGGL((attention_kernel<T, DKP>), grid, dim3(64 * nw), C::LDS, stream,
+                     static_cast<const T*>(qkv), N, heads, ldqkv, scale_log2,
+                     static_cast<T*>(out), ldo);
+  VTD_LAUNCH_CHECK("attention");
+  return VTD_OK;
+}
+
+}  // namespace
+
+int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqkv,
+                     float scale, void* out, int ldo, int dtype, hipStream_t stream,
+                     double flops) {
+  VTD_CHECK_ARG(qkv && out, "attention: null pointer");
+  VTD_CHECK_ARG(B > 0 && N > 0 && heads > 0, "attention: bad B/N/heads");
+  VTD_CHECK_ARG(dkp == 32 || dkp == 64 || dkp == 128, "attention: dkp must be 32/64/128");
+  VTD_CHECK_ARG(ldqkv >= 3 * heads * dkp && ldo >= heads * dkp,
+                "attention: leading dimensions too small");
+  VTD_CHECK_ARG(ldqkv % 8 == 0 && ldo % 8 == 0, "attention: ld must be multiple of 8");
+  VTD_CHECK_ARG(dtype == VTD_F32 || dtype == VTD_BF16, "attention: bad dtype");
+  ProfScope ps(stream, PROF_ATTN,
+               flops > 0 ? flops : 4.0 * B * heads * (double)N * N * dkp);
+  if (dtype == VTD_BF16) {
+    if (dkp == 32) return launch<bf16_t, 32>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+    if (dkp == 64) return launch<bf16_t, 64>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+    return launch<bf16_t, 128>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+  }
+  if (dkp == 32) return launch<float, 32>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+  if (dkp == 64) return launch<float, 64>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+  return launch<float, 128>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+}
+
+}  // namespace vtd
+
+extern "C" int vtd_attention(const void* qkv_dev, int B, int N, int heads, int dkp,
+                             int ldqkv, float scale, void* out_dev, int ldo, int dtype,
+                             void* stream) {
+  return vtd::attention_launch(qkv_dev, B, N, heads, dkp, ldqkv, scale, out_dev, ldo,
+                               dtype, static_cast<hipStream_t>(stream), 0.0);
+}

@@ -1,0 +1,296 @@
+// HBM-bound kernels of the forward path: LayerNorm (vtd.py:353-357, 375-379),
+// ExtractImagePatches + flatten (vtd.py:177-206, 279-280), transform_predictions
+// (vtd.py:586-647), and the one-time weight packing.
+#include "vtd_common.h"
+
+namespace vtd {
+
+namespace {
+
+// ------------------------------------------------------------------ LayerNorm
+// One wave per token row; row held in registers as NV float4 per lane -> exact
+// two-pass mean / biased variance, eps added to the variance (keras default 1e-3).
+template <typename TO, int NV>
+__global__ __launch_bounds__(256) void layernorm_kernel(
+    const float* __restrict__ x, int64_t rows, int D, int ldx,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+    TO* __restrict__ y, int ldy) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + row * ldx;
+  f32x4 v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    v[i] = c < D ? *reinterpret_cast<const f32x4*>(xr + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const float mean = s / D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if (c < D)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = v[i][j] - mean;
+        q += d * d;
+      }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+  const float rstd = 1.f / sqrtf(q / D + eps);
+  TO* yr = y + row * ldy;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if (c < D) {
+      const f32x4 g = *reinterpret_cast<const f32x4*>(gamma + c);
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(beta + c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) yr[c + j] = DT<TO>::from((v[i][j] - mean) * rstd * g[j] + bb[j]);
+    }
+  }
+  for (int c = D + lane; c < ldy; c += 64) yr[c] = DT<TO>::from(0.f);
+}
+
+// generic fallback (D % 4 != 0 or D > 4096): three passes over the row
+template <typename TO>
+__global__ __launch_bounds__(256) void layernorm_generic_kernel(
+    const float* __restrict__ x, int64_t rows, int D, int ldx,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+    TO* __restrict__ y, int ldy) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + row * ldx;
+  float s = 0.f;
+  for (int c = lane; c < D; c += 64) s += xr[c];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const float mean = s / D;
+  float q = 0.f;
+  for (int c = lane; c < D; c += 64) {
+    const float d = xr[c] - mean;
+    q += d * d;
+  }
+  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+  const float rstd = 1.f / sqrtf(q / D + eps);
+  TO* yr = y + row * ldy;
+  for (int c = lane; c < ldy; c += 64)
+    yr[c] = DT<TO>::from(c < D ? (xr[c] - mean) * rstd * gamma[c] + beta[c] : 0.f);
+}
+
+template <typename TO>
+int ln_dispatch(const float* x, int64_t rows, int D, int ldx, const float* g,
+                const float* b, float eps, void* y, int ldy, hipStream_t st) {
+  const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  TO* yo = static_cast<TO*>(y);
+  const bool vec = (D % 4 == 0) && (ldx % 4 == 0) &&
+                   (reinterpret_cast<uintptr_t>(x) % 16 == 0) &&
+                   (reinterpret_cast<uintptr_t>(g) % 16 == 0) &&
+                   (reinterpret_cast<uintptr_t>(b) % 16 == 0);
+  const int nv = (D + 255) / 256;
+  if (vec && nv <= 1)
+    hipLaunchKernelGGL((layernorm_kernel<TO, 1>), grid, block, 0, st, x, rows, D, ldx, g, b, eps, yo, ldy);
+  else if (vec && nv <= 2)
+    hipLaunchKernelGGL((layernorm_kernel<TO, 2>), grid, block, 0, st, x, rows, D, ldx, g, b, eps, yo, ldy);
+  else if (vec && nv <= 3)
+    hipLaunchKernelGGL((layernorm_kernel<TO, 3>), grid, block, 0, st, x, rows, D, ldx, g, b, eps, yo, ldy);
+  else if (vec && nv <= 4)
+    hipLaunchKernelGGL((layernorm_kernel<TO, 4>), grid, block, 0, st, x, rows, D, ldx, g, b, eps, yo, ldy);
+  else if (vec && nv <= 8)
+    hipLaunchKernelGGL((layernorm_kernel<TO, 8>), grid, block, 0, st, x, rows, D, ldx, g, b, eps, yo, ldy);
+  else if (vec && nv <= 16)
+    hipLaunchKernelGGL((layernorm_kernel<TO, 16>), grid, block, 0, st, x, rows, D, ldx, g, b, eps, yo, ldy);
+  else
+    hipLaunchKernelGGL((layernorm_generic_kernel<TO>), grid, block, 0, st, x, rows, D, ldx, g, b, eps, yo, ldy);
+  VTD_LAUNCH_CHECK("layernorm");
+  return VTD_OK;
+}
+
+// ------------------------------------------------------------------ patches
+// tf.image.extract_patches(SAME, size = stride = p) + Reshape: output row m = b*N + t
+// (t = gy*gw + gx), column k = (kh*p + kw)*C + c; outside the image -> 0.
+// Each thread writes 8 consecutive output columns (one 16-B bf16 / 32-B f32 store).
+template <typename TO>
+__global__ __launch_bounds__(256) void patches_kernel(
+    const float* __restrict__ img, int B, int H, int W, int C, int p, int gw, int N,
+    int top, int left, int P, TO* __restrict__ out, int ldo) {
+  const int chunks = ldo / 8;
+  const int64_t total = (int64_t)B * N * chunks;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = g / chunks;
+    const int k0 = (int)(g - m * chunks) * 8;
+    const int b = (int)(m / N), t = (int)(m - (int64_t)b * N);
+    const int gy = t / gw, gx = t - (t / gw) * gw;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = k0 + j;
+      float val = 0.f;
+      if (k < P) {
+        const int kh = k / (p * C), r = k - kh * p * C;
+        const int kw = r / C, c = r - kw * C;
+        const int yy = gy * p + kh - top, xx = gx * p + kw - left;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W)
+          val = img[(((int64_t)b * H + yy) * W + xx) * C + c];
+      }
+      v[j] = val;
+    }
+    TO* o = out + m * ldo + k0;
+    if constexpr (sizeof(TO) == 2) {
+      bf16x8 w;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w[j] = static_cast<short>(f32_to_bf16(v[j]));
+      *reinterpret_cast<bf16x8*>(o) = w;
+    } else {
+      *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
+      *reinterpret_cast<f32x4*>(o + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    }
+  }
+}
+
+// ------------------------------------------------------------------ decode
+// transform_predictions (vtd.py:586-647): sigmoid; clip last 4 to [0, 1];
+// [conf, cls * (CLASSES-1), cx * W, cy * H, h * H, w * W] with W = H = 608 (constant
+// Constants.MODEL_IMAGE_SIZE, not the input shape).
+__global__ void decode_kernel(const float* __restrict__ logits, int64_t n,
+                              float* __restrict__ dets) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * 6) return;
+  const int f = (int)(i % 6);
+  float s = 1.f / (1.f + expf(-logits[i]));
+  if (f >= 2) s = fminf(fmaxf(s, 0.f), 1.f);
+  const float scale = f == 0 ? 1.f : (f == 1 ? 79.f : 608.f);
+  dets[i] = s * scale;
+}
+
+// ------------------------------------------------------------------ packing
+template <typename TO>
+__global__ void pack_dense_kernel(const float* __restrict__ src, int K, int N, int kg,
+                                  int kgp, int ng, int ngp, TO* __restrict__ dst, int ld,
+                                  int off) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)K * N) return;
+  const int k = (int)(i / N), n = (int)(i - (int64_t)k * N);
+  const int kp = (k / kg) * kgp + k % kg;
+  const int np = (n / ng) * ngp + n % ng;
+  dst[(int64_t)(off + np) * ld + kp] = DT<TO>::from(src[i]);
+}
+
+__global__ void pack_vector_kernel(const float* __restrict__ src, int N, int ng, int ngp,
+                                   float* __restrict__ dst, int off) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  dst[off + (n / ng) * ngp + n % ng] = src[n];
+}
+
+}  // namespace
+
+int layernorm_launch(const float* x, int64_t rows, int D, int ldx, const float* g,
+                     const float* b, float eps, void* y, int ldy, int dtype,
+                     hipStream_t st) {
+  VTD_CHECK_ARG(x && g && b && y, "layernorm: null pointer");
+  VTD_CHECK_ARG(rows > 0 && D > 0 && ldx >= D && ldy >= D, "layernorm: bad shape");
+  VTD_CHECK_ARG(dtype == VTD_F32 || dtype == VTD_BF16, "layernorm: bad dtype");
+  ProfScope ps(st, PROF_LN, 0.0);
+  if (dtype == VTD_BF16) return ln_dispatch<bf16_t>(x, rows, D, ldx, g, b, eps, y, ldy, st);
+  return ln_dispatch<float>(x, rows, D, ldx, g, b, eps, y, ldy, st);
+}
+
+int patches_launch(const float* img, int B, int H, int W, int C, int p, void* out,
+                   int ldo, int dtype, hipStream_t st) {
+  VTD_CHECK_ARG(img && out, "extract_patches: null pointer");
+  VTD_CHECK_ARG(B > 0 && H > 0 && W > 0 && C > 0 && p > 0, "extract_patches: bad shape");
+  const int gh = (H + p - 1) / p, gw = (W + p - 1) / p;
+  const int P = p * p * C;
+  VTD_CHECK_ARG(ldo >= P && ldo % 8 == 0, "extract_patches: ld_out must be >= P, % 8");
+  VTD_CHECK_ARG(dtype == VTD_F32 || dtype == VTD_BF16, "extract_patches: bad dtype");
+  const int pad_h = (gh - 1) * p + p - H, pad_w = (gw - 1) * p + p - W;
+  const int N = gh * gw;
+  const int64_t total = (int64_t)B * N * (ldo / 8);
+  const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
+  ProfScope ps(st, PROF_PATCH, 0.0);
+  if (dtype == VTD_BF16)
+    hipLaunchKernelGGL(patches_kernel<bf16_t>, dim3(grid), dim3(256), 0, st, img, B, H, W,
+                       C, p, gw, N, pad_h / 2, pad_w / 2, P, static_cast<bf16_t*>(out), ldo);
+  else
+    hipLaunchKernelGGL(patches_kernel<float>, dim3(grid), dim3(256), 0, st, img, B, H, W,
+                       C, p, gw, N, pad_h / 2, pad_w / 2, P, static_cast<float*>(out), ldo);
+  VTD_LAUNCH_CHECK("extract_patches");
+  return VTD_OK;
+}
+
+int decode_launch(const float* logits, int64_t n, float* dets, hipStream_t st) {
+  VTD_CHECK_ARG(logits && dets && n > 0, "decode: bad args");
+  ProfScope ps(st, PROF_OTHER, 0.0);
+  const int64_t total = n * 6;
+  hipLaunchKernelGGL(decode_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                     logits, n, dets);
+  VTD_LAUNCH_CHECK("decode");
+  return VTD_OK;
+}
+
+}  // namespace vtd
+
+extern "C" {
+
+int vtd_layernorm(const float* x_dev, int64_t rows, int D, int ldx, const float* gamma_dev,
+                  const float* beta_dev, float eps, void* y_dev, int ldy, int dtype,
+                  void* stream) {
+  return vtd::layernorm_launch(x_dev, rows, D, ldx, gamma_dev, beta_dev, eps, y_dev, ldy,
+                               dtype, static_cast<hipStream_t>(stream));
+}
+
+int vtd_extract_patches(const float* images_dev, int B, int H, int W, int C, int p,
+                        void* out_dev, int ld_out, int dtype, void* stream) {
+  return vtd::patches_launch(images_dev, B, H, W, C, p, out_dev, ld_out, dtype,
+                             static_cast<hipStream_t>(stream));
+}
+
+int vtd_decode(const float* logits_dev, int64_t n, float* dets_dev, void* stream) {
+  return vtd::decode_launch(logits_dev, n, dets_dev, static_cast<hipStream_t>(stream));
+}
+
+int vtd_pack_dense(const float* src_dev, int K, int N, int k_group, int k_group_p,
+                   int n_group, int n_group_p, void* dst_dev, int ld_dst, int n_row_offset,
+                   int dtype, void* stream) {
+  VTD_CHECK_ARG(src_dev && dst_dev && K > 0 && N > 0, "pack_dense: bad args");
+  VTD_CHECK_ARG(k_group > 0 && k_group_p >= k_group && n_group > 0 && n_group_p >= n_group,
+                "pack_dense: bad groups");
+  VTD_CHECK_ARG((K / k_group - 1) * k_group_p + k_group <= ld_dst,
+                "pack_dense: ld_dst too small");
+  const int64_t total = (int64_t)K * N;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (dtype == VTD_BF16)
+    hipLaunchKernelGGL(vtd::pack_dense_kernel<vtd::bf16_t>, grid, dim3(256), 0, st, src_dev,
+                       K, N, k_group, k_group_p, n_group, n_group_p,
+                       static_cast<vtd::bf16_t*>(dst_dev), ld_dst, n_row_offset);
+  else if (dtype == VTD_F32)
+    hipLaunchKernelGGL(vtd::pack_dense_kernel<float>, grid, dim3(256), 0, st, src_dev, K, N,
+                       k_group, k_group_p, n_group, n_group_p, static_cast<float*>(dst_dev),
+                       ld_dst, n_row_offset);
+  else
+    return vtd::fail(VTD_ERR_UNSUPPORTED, "pack_dense: bad dtype");
+  VTD_LAUNCH_CHECK("pack_dense");
+  return VTD_OK;
+}
+
+int vtd_pack_vector(const float* src_dev, int N, int n_group, int n_group_p, float* dst_dev,
+                    int offset, void* stream) {
+  VTD_CHECK_ARG(src_dev && dst_dev && N > 0 && n_group > 0 && n_group_p >= n_group,
+                "pack_vector: bad args");
+  hipLaunchKernelGGL(vtd::pack_vector_kernel, dim3((N + 255) / 256), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), src_dev, N, n_group, n_group_p,
+                     dst_dev, offset);
+  VTD_LAUNCH_CHECK("pack_vector");
+  return VTD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,361 @@
+// Host runtime of libvtd.so: error state, graph shapes, workspace plan, the whole
+// forward (`model(images, training=False)`, vtd.py:498-583) as one sequence of
+// launches on the caller's stream, and optional hipEvent per-launch profiling.
+#include <algorithm>
+#include <cmath>
+#include <mutex>
+#include <vector>
+
+#include "vtd_common.h"
+
+namespace vtd {
+
+int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
+                int dtype, const vtd_epilogue* epi, hipStream_t stream, double flops);
+int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqkv,
+                     float scale, void* out, int ldo, int dtype, hipStream_t stream,
+                     double flops);
+int layernorm_launch(const float* x, int64_t rows, int D, int ldx, const float* g,
+                     const float* b, float eps, void* y, int ldy, int dtype, hipStream_t st);
+int patches_launch(const float* img, int B, int H, int W, int C, int p, void* out, int ldo,
+                   int dtype, hipStream_t st);
+int decode_launch(const float* logits, int64_t n, float* dets, hipStream_t st);
+
+// ------------------------------------------------------------------ errors
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+// ------------------------------------------------------------------ profiling
+namespace {
+struct ProfRecord { int cls; int ev0, ev1; double flops; };
+struct ProfState {
+  std::mutex mu;
+  bool enabled = false;
+  std::vector<hipEvent_t> events;
+  int next_event = 0;
+  std::vector<ProfRecord> pending;
+  double ms[VTD_PROF_CLASSES] = {0};
+  int64_t launches[VTD_PROF_CLASSES] = {0};
+  double flops[VTD_PROF_CLASSES] = {0};
+};
+ProfState& prof() {
+  static ProfState s;
+  return s;
+}
+int prof_event() {  // caller holds the mutex
+  ProfState& p = prof();
+  if (p.next_event == (int)p.events.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return -1;
+    p.events.push_back(e);
+  }
+  return p.next_event++;
+}
+}  // namespace
+
+ProfScope::ProfScope(hipStream_t s, int c, double fl) : stream(s), cls(c), slot(-1) {
+  ProfState& p = prof();
+  if (!p.enabled) return;
+  std::lock_guard<std::mutex> g(p.mu);
+  int e0 = prof_event(), e1 = prof_event();
+  if (e0 < 0 || e1 < 0) return;
+  (void)hipEventRecord(p.events[e0], stream);
+  p.pending.push_back({c, e0, e1, fl});
+  slot = (int)p.pending.size() - 1;
+}
+ProfScope::~ProfScope() {
+  if (slot < 0) return;
+  ProfState& p = prof();
+  std::lock_guard<std::mutex> g(p.mu);
+  (void)hipEventRecord(p.events[p.pending[slot].ev1], stream);
+}
+
+// ------------------------------------------------------------------ shapes
+static int derive(const vtd_config* c, vtd_dims* d) {
+  VTD_CHECK_ARG(c && d, "null config/dims");
+  VTD_CHECK_ARG(c->batch > 0 && c->image_h > 0 && c->image_w > 0 && c->channels > 0,
+                "batch and input_shape must be positive");
+  VTD_CHECK_ARG(c->patch_size > 0 && c->embedding_dim > 0 && c->num_heads > 0 &&
+                    c->key_dim > 0 && c->mlp_quantities > 0 && c->repeat_times > 0,
+                "patch_size, embedding_dim, heads, key_dim, mlp/repeat counts must be > 0");
+  VTD_CHECK_ARG(c->mlp_quantities <= VTD_MAX_MLP, "encoder_mlp_quantities too large");
+  VTD_CHECK_ARG(c->head_last_units > 0 && c->head_layers > 0 && c->head_repeats > 0 &&
+                    c->head_layers * c->head_repeats <= VTD_MAX_HEAD,
+                "bad mlp_head configuration");
+  VTD_CHECK_ARG(c->dtype == VTD_F32 || c->dtype == VTD_BF16, "dtype must be F32 or BF16");
+  VTD_CHECK_ARG(c->key_dim <= 128, "encoder_key_dim > 128 not supported");
+  const int p = c->patch_size;
+  d->grid_h = (c->image_h + p - 1) / p;
+  d->grid_w = (c->image_w + p - 1) / p;
+  d->tokens = d->grid_h * d->grid_w;
+  d->pad_top = ((d->grid_h - 1) * p + p - c->image_h) / 2;
+  d->pad_left = ((d->grid_w - 1) * p + p - c->image_w) / 2;
+  d->patch_dim = p * p * c->channels;
+  d->patch_dim_p = (int)round_up(d->patch_dim, VTD_KALIGN);
+  d->d = c->embedding_dim;
+  d->d_p = (int)round_up(d->d, VTD_KALIGN);
+  int dkp = c->key_dim <= 32 ? 32 : (c->key_dim <= 64 ? 64 : 128);
+  if ((c->num_heads * dkp) % VTD_KALIGN) dkp *= 2;
+  VTD_CHECK_ARG(dkp <= 128, "key_dim padding exceeds 128");
+  d->key_dim_p = dkp;
+  d->inner_p = c->num_heads * dkp;
+  d->qkv_p = (int)round_up(3 * d->inner_p, VTD_KALIGN);
+  for (int j = 0; j < VTD_MAX_MLP; ++j) d->mlp_units[j] = d->mlp_units_p[j] = 0;
+  for (int j = 0; j < c->mlp_quantities; ++j) {      // vtd.py:385-386
+    const int64_t u = (int64_t)d->d << (c->mlp_quantities - 1 - j);
+    VTD_CHECK_ARG(u < (1 << 24), "encoder MLP width overflow");
+    d->mlp_units[j] = (int)u;
+    d->mlp_units_p[j] = (int)round_up(u, VTD_KALIGN);
+  }
+  d->n_head = c->head_layers * c->head_repeats;
+  for (int j = 0; j < VTD_MAX_HEAD; ++j) d->head_units[j] = d->head_units_p[j] = 0;
+  int idx = 0;
+  for (int e = c->head_layers - 1; e >= 0; --e) {     // vtd.py:465-470
+    const int64_t u = (int64_t)c->head_last_units << e;
+    VTD_CHECK_ARG(u < (1 << 24), "head width overflow");
+    for (int r = 0; r < c->head_repeats; ++r, ++idx) {
+      d->head_units[idx] = (int)u;
+      d->head_units_p[idx] = (int)round_up(u, VTD_KALIGN);
+    }
+  }
+  d->tokens_p = (int)round_up(d->tokens, VTD_KALIGN);
+  d->rows = (int64_t)c->batch * d->tokens;
+  d->head_rows = (int64_t)c->batch * VTD_MAX_DETECT;
+  return VTD_OK;
+}
+
+namespace {
+struct Plan {
+  size_t patches, x, xb, h, qkv, attn, mlp0, mlp1, u, head0, head1, total;
+};
+size_t es_of(int dtype) { return dtype == VTD_BF16 ? 2 : 4; }
+Plan make_plan(const vtd_config* c, const vtd_dims& d) {
+  Plan p{};
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += (bytes + 255) / 256 * 256;
+    return o;
+  };
+  const size_t es = es_of(c->dtype);
+  const size_t R = (size_t)d.rows, HR = (size_t)d.head_rows;
+  int mlp_max = 0, head_max = 0;
+  for (int j = 0; j < c->mlp_quantities; ++j) mlp_max = std::max(mlp_max, d.mlp_units_p[j]);
+  for (int j = 0; j < d.n_head; ++j) head_max = std::max(head_max, d.head_units_p[j]);
+  p.patches = take(R * d.patch_dim_p * es);
+  p.x = take(R * d.d_p * 4);
+  p.xb = take(c->dtype == VTD_BF16 ? R * d.d_p * 2 : 0);
+  p.h = take(R * d.d_p * es);
+  p.qkv = take(R * d.qkv_p * es);
+  p.attn = take(R * d.inner_p * es);
+  p.mlp0 = take(R * mlp_max * es);
+  p.mlp1 = take(R * mlp_max * es);
+  p.u = take(HR * d.tokens_p * es);
+  p.head0 = take(HR * head_max * es);
+  p.head1 = take(HR * head_max * es);
+  p.total = off;
+  return p;
+}
+}  // namespace
+
+}  // namespace vtd
+
+using namespace vtd;
+
+extern "C" {
+
+int vtd_abi_version(void) { return VTD_ABI_VERSION; }
+const char* vtd_last_error(void) { return g_last_error.c_str(); }
+
+int vtd_derive_dims(const vtd_config* cfg, vtd_dims* out) { return derive(cfg, out); }
+
+int vtd_workspace_bytes(const vtd_config* cfg, size_t* bytes) {
+  VTD_CHECK_ARG(bytes, "null bytes pointer");
+  vtd_dims d;
+  int rc = derive(cfg, &d);
+  if (rc) return rc;
+  *bytes = make_plan(cfg, d).total;
+  return VTD_OK;
+}
+
+int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images,
+                float* logits, float* dets, void* workspace, size_t workspace_bytes,
+                void* stream_) {
+  vtd_dims d;
+  int rc = derive(cfg, &d);
+  if (rc) return rc;
+  VTD_CHECK_ARG(w && images && logits && workspace, "forward: null pointer");
+  VTD_CHECK_ARG(w->layers, "forward: weights.layers is null");
+  const Plan P = make_plan(cfg, d);
+  if (workspace_bytes < P.total)
+    return fail(VTD_ERR_WORKSPACE, "forward: workspace too small (need " +
+                                       std::to_string(P.total) + " bytes)");
+  hipStream_t st = static_cast<hipStream_t>(stream_);
+  char* ws = static_cast<char*>(workspace);
+  const int dt = cfg->dtype;
+  const int B = cfg->batch, N = d.tokens, D = d.d, Dp = d.d_p;
+  const int64_t R = d.rows;
+  VTD_CHECK_ARG(R < (int64_t)1 << 31, "forward: batch*tokens too large");
+  const int M = (int)R;
+  void* patches = ws + P.patches;
+  float* x = reinterpret_cast<float*>(ws + P.x);
+  void* xb = ws + P.xb;
+  void* h = ws + P.h;
+  void* qkv = ws + P.qkv;
+  void* attn = ws + P.attn;
+  void* mlp[2] = {ws + P.mlp0, ws + P.mlp1};
+  void* u = ws + P.u;
+  void* head[2] = {ws + P.head0, ws + P.head1};
+  const int act = cfg->use_mish ? VTD_ACT_MISH : VTD_ACT_GELU_TANH;
+  const double fR = (double)R;
+
+  // ---- ExtractImagePatches + flatten (vtd.py:271-280)
+  rc = patches_launch(images, B, cfg->image_h, cfg->image_w, cfg->channels,
+                      cfg->patch_size, patches, d.patch_dim_p, dt, st);
+  if (rc) return rc;
+  // ---- linear_projection + position embedding add (vtd.py:291-307)
+  {
+    vtd_epilogue e{};
+    e.bias = w->b_patch;
+    e.rowadd = w->pos_embedding; e.rowadd_period = N; e.rowadd_ncols = D;
+    e.act = VTD_ACT_NONE;
+    e.out = x; e.ldo = Dp; e.out_dtype = VTD_F32;
+    rc = gemm_launch(M, Dp, d.patch_dim_p, patches, d.patch_dim_p, w->w_patch,
+                     d.patch_dim_p, dt, &e, st, 2.0 * fR * D * d.patch_dim);
+    if (rc) return rc;
+  }
+  const int q = cfg->mlp_quantities;
+  const float scale = 1.0f / std::sqrt((float)cfg->key_dim);
+  for (int i = 0; i < cfg->repeat_times; ++i) {        // vtd.py:350-412
+    const vtd_layer_weights& L = w->layers[i];
+    rc = layernorm_launch(x, R, D, Dp, L.ln1_gamma, L.ln1_beta, 1e-3f, h, Dp, dt, st);
+    if (rc) return rc;
+    {
+      vtd_epilogue e{};
+      e.bias = L.b_qkv; e.act = VTD_ACT_NONE;
+      e.out = qkv; e.ldo = d.qkv_p; e.out_dtype = dt;
+      rc = gemm_launch(M, d.qkv_p, Dp, h, Dp, L.w_qkv, Dp, dt, &e, st,
+                       2.0 * fR * D * 3.0 * cfg->num_heads * cfg->key_dim);
+      if (rc) return rc;
+    }
+    rc = attention_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale, attn,
+                          d.inner_p, dt, st,
+                          4.0 * B * cfg->num_heads * (double)N * N * cfg->key_dim);
+    if (rc) return rc;
+    {
+      vtd_epilogue e{};
+      e.bias = L.b_out; e.act = VTD_ACT_NONE;
+      e.resid = x; e.ldr = Dp;
+      e.out = x; e.ldo = Dp; e.out_dtype = VTD_F32;
+      rc = gemm_launch(M, Dp, d.inner_p, attn, d.inner_p, L.w_out, d.inner_p, dt, &e, st,
+                       2.0 * fR * cfg->num_heads * cfg->key_dim * D);
+      if (rc) return rc;
+    }
+    rc = layernorm_launch(x, R, D, Dp, L.ln2_gamma, L.ln2_beta, 1e-3f, h, Dp, dt, st);
+    if (rc) return rc;
+    const void* a = h;
+    int k = Dp, kv = D;
+    for (int j = 0; j < q; ++j) {
+      const bool last = j == q - 1;
+      vtd_epilogue e{};
+      e.bias = L.b_mlp[j]; e.act = act;
+      if (last) {
+        e.resid = x; e.ldr = Dp;
+        e.out = x; e.ldo = Dp; e.out_dtype = VTD_F32;
+        if (i == cfg->repeat_times - 1 && dt == VTD_BF16) { e.out2 = xb; e.ldo2 = Dp; }
+      } else {
+        e.out = mlp[j & 1]; e.ldo = d.mlp_units_p[j]; e.out_dtype = dt;
+      }
+      rc = gemm_launch(M, d.mlp_units_p[j], k, a, k, L.w_mlp[j], k, dt, &e, st,
+                       2.0 * fR * kv * d.mlp_units[j]);
+      if (rc) return rc;
+      a = mlp[j & 1];
+      k = d.mlp_units_p[j];
+      kv = d.mlp_units[j];
+    }
+  }
+  // ---- mlp_head: Dense(17) + Reshape((17, -1)) as a scatter epilogue (vtd.py:454-463)
+  {
+    const size_t es = es_of(dt);
+    VTD_HIP(hipMemsetAsync(u, 0, (size_t)d.head_rows * d.tokens_p * es, st));
+    vtd_epilogue e{};
+    e.bias = w->b_det; e.act = VTD_ACT_NONE;
+    e.out = u; e.ldo = d.tokens_p; e.out_dtype = dt;
+    e.scatter_tokens = N;
+    const void* a = dt == VTD_BF16 ? xb : static_cast<const void*>(x);
+    rc = gemm_launch(M, VTD_MAX_DETECT, Dp, a, Dp, w->w_det, Dp, dt, &e, st,
+                     2.0 * fR * D * VTD_MAX_DETECT);
+    if (rc) return rc;
+  }
+  const int HR = (int)d.head_rows;
+  const void* a = u;
+  int k = d.tokens_p, kv = N;
+  for (int j = 0; j < d.n_head; ++j) {                // vtd.py:468-486
+    vtd_epilogue e{};
+    e.bias = w->b_head[j]; e.act = act;
+    e.out = head[j & 1]; e.ldo = d.head_units_p[j]; e.out_dtype = dt;
+    rc = gemm_launch(HR, d.head_units_p[j], k, a, k, w->w_head[j], k, dt, &e, st,
+                     2.0 * HR * (double)kv * d.head_units[j]);
+    if (rc) return rc;
+    a = head[j & 1];
+    k = d.head_units_p[j];
+    kv = d.head_units[j];
+  }
+  {                                                   // MLP_Head_no_Sigmoid vtd.py:489-493
+    vtd_epilogue e{};
+    e.bias = w->b_final; e.act = VTD_ACT_NONE;
+    e.out = logits; e.ldo = 6; e.out_dtype = VTD_F32;
+    rc = gemm_launch(HR, 6, k, a, k, w->w_final, k, dt, &e, st, 2.0 * HR * (double)kv * 6);
+    if (rc) return rc;
+  }
+  if (dets) {
+    rc = decode_launch(logits, d.head_rows, dets, st);
+    if (rc) return rc;
+  }
+  return VTD_OK;
+}
+
+int vtd_profile_enable(int enable) {
+  ProfState& p = prof();
+  std::lock_guard<std::mutex> g(p.mu);
+  p.enabled = enable != 0;
+  return VTD_OK;
+}
+
+int vtd_profile_reset(void) {
+  ProfState& p = prof();
+  std::lock_guard<std::mutex> g(p.mu);
+  for (auto& r : p.pending) (void)hipEventSynchronize(p.events[r.ev1]);
+  p.pending.clear();
+  p.next_event = 0;
+  for (int i = 0; i < VTD_PROF_CLASSES; ++i) p.ms[i] = 0, p.launches[i] = 0, p.flops[i] = 0;
+  return VTD_OK;
+}
+
+int vtd_profile_read(double* ms, int64_t* launches, double* flops, int n_classes) {
+  ProfState& p = prof();
+  std::lock_guard<std::mutex> g(p.mu);
+  for (auto& r : p.pending) {
+    hipError_t e = hipEventSynchronize(p.events[r.ev1]);
+    if (e != hipSuccess) return fail(VTD_ERR_HIP, std::string("profile: ") + hipGetErrorString(e));
+    float t = 0.f;
+    (void)hipEventElapsedTime(&t, p.events[r.ev0], p.events[r.ev1]);
+    p.ms[r.cls] += t;
+    p.launches[r.cls] += 1;
+    p.flops[r.cls] += r.flops;
+  }
+  p.pending.clear();
+  p.next_event = 0;
+  for (int i = 0; i < n_classes && i < VTD_PROF_CLASSES; ++i) {
+    if (ms) ms[i] = p.ms[i];
+    if (launches) launches[i] = p.launches[i];
+    if (flops) flops[i] = p.flops[i];
+  }
+  return VTD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,404 @@
+"""Host-side mirror of the reference model API, backed by libvtd.so.
+
+Reference: /root/reference/vision_transformer_detector.py (cited vtd.py:N).
+  create_vision_transformer_detector(...)   vtd.py:498-583  -> Model
+  Model.__call__(images, training=False)    keras.Model call (vtd.py:331-335)
+  Model.predict(images, batch_size=32)      keras.Model.predict (ipynb:836)
+  Model.get_weights() / set_weights()       keras (vtd.py:2155-2157), Keras layer names
+  transform_predictions(logits)             vtd.py:586-647
+  Constants                                 vtd.py:19-43
+
+Every compute call goes through the C-ABI (`_lib`); there is no CPU/torch fallback.
+Caller-visible layout is the reference's: NHWC fp32 images in [-1, 1] in, (B, 17, 6)
+fp32 pre-sigmoid logits out.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from collections import OrderedDict
+from enum import Enum
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+
+class Constants(Enum):                                   # vtd.py:19-43
+    CLASSES = 80
+    MODEL_IMAGE_SIZE = 608, 608
+    EPSILON = 1e-8
+    MAX_DETECT_OBJECTS_QUANTITY = 17
+    LATEST_RELATED_IMAGES = 3
+    BBOXES_PER_IMAGE = 14
+    OBJECTNESS_THRESHOLD = 0.5
+    CLASSIFICATION_CONFIDENCE_THRESHOLD = 0.5
+
+
+_DTYPES = {"float32": L.F32, "fp32": L.F32, "f32": L.F32, "bfloat16": L.BF16,
+           "bf16": L.BF16}
+_TORCH_DTYPE = {L.F32: torch.float32, L.BF16: torch.bfloat16}
+
+
+def _resolve_dtype(dtype) -> int:
+    if isinstance(dtype, torch.dtype):
+        dtype = {torch.float32: "f32", torch.bfloat16: "bf16"}.get(dtype, str(dtype))
+    try:
+        return _DTYPES[str(dtype).lower()]
+    except KeyError:
+        raise ValueError(f"unsupported dtype {dtype!r}: use 'float32' (parity) or 'bfloat16'")
+
+
+# ------------------------------------------------------------------------- names
+def keras_weight_names(kw: dict, dims: L.VtdDims) -> "OrderedDict[str, tuple]":
+    """Keras weight name -> shape of the graph vtd.py:498-583 builds (after
+    keras.backend.clear_session(), vtd.py:548, layer names are deterministic)."""
+    d, nh, dk = kw["embedding_dim"], kw["encoder_num_heads"], kw["encoder_key_dim"]
+    out = OrderedDict()
+    out["position_encoding/position_embedding/embeddings"] = (dims.tokens, 1)
+    out["linear_projection/kernel"] = (dims.patch_dim, d)
+    out["linear_projection/bias"] = (d,)
+    q = kw["encoder_mlp_quantities"]
+    for i in range(1, kw["encoder_repeat_times"] + 1):
+        ln1 = "layer_normalization" if i == 1 else f"layer_normalization_{2 * i - 2}"
+        ln2 = f"layer_normalization_{2 * i - 1}"
+        mha = "multi_head_attention" if i == 1 else f"multi_head_attention_{i - 1}"
+        out[f"{ln1}/gamma"] = (d,)
+        out[f"{ln1}/beta"] = (d,)
+        for part in ("query", "key", "value"):
+            out[f"{mha}/{part}/kernel"] = (d, nh, dk)
+            out[f"{mha}/{part}/bias"] = (nh, dk)
+        out[f"{mha}/attention_output/kernel"] = (nh, dk, d)
+        out[f"{mha}/attention_output/bias"] = (d,)
+        out[f"{ln2}/gamma"] = (d,)
+        out[f"{ln2}/beta"] = (d,)
+        k = d
+        for j in range(q):
+            n = dims.mlp_units[j]
+            out[f"MLP_{i}_{j + 1}/kernel"] = (k, n)
+            out[f"MLP_{i}_{j + 1}/bias"] = (n,)
+            k = n
+    out["dense/kernel"] = (d, L.MAX_DETECT)
+    out["dense/bias"] = (L.MAX_DETECT,)
+    k = dims.tokens
+    for j in range(dims.n_head):
+        n = dims.head_units[j]
+        out[f"dense_{j + 1}/kernel"] = (k, n)
+        out[f"dense_{j + 1}/bias"] = (n,)
+        k = n
+    out["MLP_Head_no_Sigmoid/kernel"] = (k, 6)
+    out["MLP_Head_no_Sigmoid/bias"] = (6,)
+    return out
+
+
+def _glorot_fans(shape):
+    if len(shape) == 2:
+        return shape[0], shape[1]
+    rf = int(np.prod(shape[:-2]))
+    return shape[-2] * rf, shape[-1] * rf
+
+
+def keras_default_init(names: "OrderedDict[str, tuple]", seed: int = 0):
+    """Keras defaults [upstream]: glorot_uniform kernels, zero biases, LN gamma=1 beta=0,
+    Embedding U(-0.05, 0.05).  Returns fp32 CPU tensors."""
+    g = torch.Generator().manual_seed(seed)
+    out = OrderedDict()
+    for name, shape in names.items():
+        if name.endswith("/embeddings"):
+            t = torch.rand(shape, generator=g) * 0.1 - 0.05
+        elif name.endswith("/kernel"):
+            fi, fo = _glorot_fans(shape)
+            lim = math.sqrt(6.0 / (fi + fo))
+            t = torch.rand(shape, generator=g) * (2 * lim) - lim
+        elif name.endswith("/gamma"):
+            t = torch.ones(shape)
+        else:
+            t = torch.zeros(shape)
+        out[name] = t.float()
+    return out
+
+
+# ------------------------------------------------------------------------- model
+class Model:
+    """Inference model equivalent to the keras.Model `vision_transformer_detector`."""
+
+    name = "vision_transformer_detector"
+
+    def __init__(self, kwargs: dict, dtype=torch.bfloat16, device=None, seed: int = 0):
+        self.kwargs = dict(kwargs)
+        self.dtype = _resolve_dtype(dtype)
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.type != "cuda":
+            raise ValueError("Model runs on a HIP device only (device='cuda[:i]')")
+        h, w, c = self.kwargs["input_shape"]
+        self.input_shape = (int(h), int(w), int(c))
+        self._cfg_template = dict(
+            image_h=h, image_w=w, channels=c, patch_size=self.kwargs["patch_size"],
+            embedding_dim=self.kwargs["embedding_dim"],
+            num_heads=self.kwargs["encoder_num_heads"], key_dim=self.kwargs["encoder_key_dim"],
+            mlp_quantities=self.kwargs["encoder_mlp_quantities"],
+            repeat_times=self.kwargs["encoder_repeat_times"],
+            head_last_units=self.kwargs["mlp_head_last_units"],
+            head_layers=self.kwargs["mlp_head_dense_layers_quantity"],
+            head_repeats=self.kwargs["mlp_head_dense_mish_block_repeats"],
+            use_mish=1 if self.kwargs["use_mish"] else 0, dtype=self.dtype)
+        self.dims = self._derive(1)
+        self.weight_shapes = keras_weight_names(self.kwargs, self.dims)
+        self._master = None            # fp32 CPU tensors keyed by Keras name
+        self._packed = []              # keeps device buffers alive
+        self._ws = None
+        self._ws_bytes = 0
+        self.set_weights(keras_default_init(self.weight_shapes, seed))
+
+    # ---- config helpers
+    def config(self, batch: int) -> L.VtdConfig:
+        return L.VtdConfig(batch=int(batch), **self._cfg_template)
+
+    def _derive(self, batch: int) -> L.VtdDims:
+        cfg, dims = self.config(batch), L.VtdDims()
+        L.check(L.lib.vtd_derive_dims(ctypes.byref(cfg), ctypes.byref(dims)), "derive_dims")
+        return dims
+
+    def workspace_bytes(self, batch: int) -> int:
+        cfg, n = self.config(batch), ctypes.c_size_t()
+        L.check(L.lib.vtd_workspace_bytes(ctypes.byref(cfg), ctypes.byref(n)), "workspace")
+        return int(n.value)
+
+    # ---- weights
+    def get_weights(self):
+        """Weights as a list in Keras creation order (names: `weight_names()`)."""
+        return [self._master[n].numpy().copy() for n in self.weight_shapes]
+
+    def weight_names(self):
+        return list(self.weight_shapes)
+
+    def get_weight_dict(self):
+        return OrderedDict((n, self._master[n].numpy().copy()) for n in self.weight_shapes)
+
+    def set_weights(self, weights):
+        """Accepts a dict keyed by Keras weight names or a list in `weight_names()` order."""
+        if isinstance(weights, dict):
+            missing = [n for n in self.weight_shapes if n not in weights]
+            extra = [n for n in weights if n not in self.weight_shapes]
+            if missing or extra:
+                raise ValueError(f"set_weights: missing {missing[:5]} unexpected {extra[:5]}")
+            items = [(n, weights[n]) for n in self.weight_shapes]
+        else:
+            weights = list(weights)
+            if len(weights) != len(self.weight_shapes):
+                raise ValueError(f"set_weights: expected {len(self.weight_shapes)} arrays, "
+                                 f"got {len(weights)}")
+            items = list(zip(self.weight_shapes, weights))
+        master = OrderedDict()
+        for n, v in items:
+            t = torch.as_tensor(np.asarray(v) if not torch.is_tensor(v) else v).float().cpu()
+            if tuple(t.shape) != tuple(self.weight_shapes[n]):
+                raise ValueError(f"set_weights: {n} has shape {tuple(t.shape)}, expected "
+                                 f"{self.weight_shapes[n]}")
+            master[n] = t.contiguous()
+        self._master = master
+        self._pack()
+
+    def _pack(self):
+        dims, dt = self.dims, self.dtype
+        tdt = _TORCH_DTYPE[dt]
+        dev = self.device
+        keep, staging = [], []
+        stream = L.stream_ptr(torch.cuda.current_stream(dev))
+
+        def zeros(*shape, dtype=tdt):
+            t = torch.zeros(shape, dtype=dtype, device=dev)
+            keep.append(t)
+            return t
+
+        def src(name):
+            t = self._master[name].to(dev).contiguous()
+            staging.append(t)
+            return t
+
+        def dense(name, rows_p, k_p, kg=None, kgp=None, ng=None, ngp=None, dst=None, off=0):
+            w = src(name + "/kernel")
+            w2 = w.reshape(-1, w.shape[-1]) if w.dim() == 3 and kg is not None else w.reshape(w.shape[0], -1)
+            K, N = w2.shape
+            if dst is None:
+                dst = zeros(rows_p, k_p)
+            L.check(L.lib.vtd_pack_dense(w2.data_ptr(), K, N, kg or K, kgp or K, ng or N,
+                                         ngp or N, dst.data_ptr(), k_p, off, dt, stream),
+                    f"pack {name}")
+            return dst
+
+        def vector(name, n_p, ng=None, ngp=None, dst=None, off=0):
+            v = src(name).reshape(-1)
+            if dst is None:
+                dst = zeros(n_p, dtype=torch.float32)
+            N = v.numel()
+            L.check(L.lib.vtd_pack_vector(v.data_ptr(), N, ng or N, ngp or N, dst.data_ptr(),
+                                          off, stream), f"pack {name}")
+            return dst
+
+        kw = self.kwargs
+        dk, dkp = kw["encoder_key_dim"], dims.key_dim_p
+        W = L.VtdWeights()
+        W.w_patch = dense("linear_projection", dims.d_p, dims.patch_dim_p).data_ptr()
+        W.b_patch = vector("linear_projection/bias", dims.d_p).data_ptr()
+        pos = src("position_encoding/position_embedding/embeddings").reshape(-1)
+        keep.append(pos)
+        W.pos_embedding = pos.data_ptr()
+        nl = kw["encoder_repeat_times"]
+        layers = (L.VtdLayerWeights * nl)()
+        for i in range(1, nl + 1):
+            ln1 = "layer_normalization" if i == 1 else f"layer_normalization_{2 * i - 2}"
+            ln2 = f"layer_normalization_{2 * i - 1}"
+            mha = "multi_head_attention" if i == 1 else f"multi_head_attention_{i - 1}"
+            Ly = layers[i - 1]
+            Ly.ln1_gamma = vector(f"{ln1}/gamma", dims.d_p).data_ptr()
+            Ly.ln1_beta = vector(f"{ln1}/beta", dims.d_p).data_ptr()
+            Ly.ln2_gamma = vector(f"{ln2}/gamma", dims.d_p).data_ptr()
+            Ly.ln2_beta = vector(f"{ln2}/beta", dims.d_p).data_ptr()
+            wqkv = zeros(dims.qkv_p, dims.d_p)
+            bqkv = zeros(dims.qkv_p, dtype=torch.float32)
+            for part_i, part in enumerate(("query", "key", "value")):
+                off = part_i * dims.inner_p
+                # EinsumDense kernel (D, H, dk) -> (D, H*dk); columns padded per head
+                dense(f"{mha}/{part}", None, dims.d_p, ng=dk, ngp=dkp, dst=wqkv, off=off)
+                vector(f"{mha}/{part}/bias", None, ng=dk, ngp=dkp, dst=bqkv, off=off)
+            Ly.w_qkv, Ly.b_qkv = wqkv.data_ptr(), bqkv.data_ptr()
+            # attention_output kernel (H, dk, D) -> (H*dk, D); rows padded per head
+            Ly.w_out = dense(f"{mha}/attention_output", dims.d_p, dims.inner_p, kg=dk,
+                             kgp=dkp).data_ptr()
+            Ly.b_out = vector(f"{mha}/attention_output/bias", dims.d_p).data_ptr()
+            k_p = dims.d_p
+            for j in range(kw["encoder_mlp_quantities"]):
+                n_p = dims.mlp_units_p[j]
+                Ly.w_mlp[j] = dense(f"MLP_{i}_{j + 1}", n_p, k_p).data_ptr()
+                Ly.b_mlp[j] = vector(f"MLP_{i}_{j + 1}/bias", n_p).data_ptr()
+                k_p = n_p
+        W.layers = ctypes.cast(layers, ctypes.POINTER(L.VtdLayerWeights))
+        W.w_det = dense("dense", L.KALIGN, dims.d_p).data_ptr()
+        W.b_det = vector("dense/bias", L.KALIGN).data_ptr()
+        k_p = dims.tokens_p
+        for j in range(dims.n_head):
+            n_p = dims.head_units_p[j]
+            W.w_head[j] = dense(f"dense_{j + 1}", n_p, k_p).data_ptr()
+            W.b_head[j] = vector(f"dense_{j + 1}/bias", n_p).data_ptr()
+            k_p = n_p
+        W.w_final = dense("MLP_Head_no_Sigmoid", L.KALIGN, k_p).data_ptr()
+        W.b_final = vector("MLP_Head_no_Sigmoid/bias", L.KALIGN).data_ptr()
+        torch.cuda.current_stream(dev).synchronize()
+        del staging      # fp32 staging copies; the packed buffers stay alive in `keep`
+        self._packed = keep
+        self._layers_c = layers
+        self._weights_c = W
+
+    # ---- forward
+    def _workspace(self, batch: int):
+        need = self.workspace_bytes(batch)
+        if self._ws is None or self._ws_bytes < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+            self._ws_bytes = need
+        return self._ws
+
+    def _as_images(self, images) -> torch.Tensor:
+        x = images if torch.is_tensor(images) else torch.as_tensor(np.asarray(images))
+        if x.dim() != 4 or tuple(x.shape[1:]) != self.input_shape:
+            raise ValueError(
+                f"Input 0 of layer \"{self.name}\" is incompatible with the layer: expected "
+                f"shape=(None, {', '.join(map(str, self.input_shape))}), found shape="
+                f"{tuple(x.shape)}")
+        return x.to(device=self.device, dtype=torch.float32).contiguous()
+
+    def forward(self, images, with_detections: bool = False, stream=None):
+        x = self._as_images(images)
+        b = x.shape[0]
+        logits = torch.empty((b, L.MAX_DETECT, 6), dtype=torch.float32, device=self.device)
+        dets = torch.empty_like(logits) if with_detections else None
+        ws = self._workspace(b)
+        cfg = self.config(b)
+        with torch.cuda.device(self.device):
+            st = L.stream_ptr(stream)
+            L.check(L.lib.vtd_forward(ctypes.byref(cfg), ctypes.byref(self._weights_c),
+                                      x.data_ptr(), logits.data_ptr(), L.ptr(dets),
+                                      ws.data_ptr(), ws.numel(), st), "vtd_forward")
+        return (logits, dets) if with_detections else logits
+
+    def __call__(self, images, training=None, **_):
+        if training:
+            raise ValueError("this forward path is inference-only (training=False)")
+        return self.forward(images)
+
+    def detect(self, images):
+        """(logits, transform_predictions(logits)) with the decode fused on device."""
+        return self.forward(images, with_detections=True)
+
+    def predict(self, x, batch_size: int = 32, verbose=0):
+        """keras.Model.predict: numpy in, numpy (N, 17, 6) logits out, batches of 32."""
+        x = np.asarray(x, dtype=np.float32)
+        outs = []
+        for i in range(0, x.shape[0], batch_size):
+            outs.append(self.forward(x[i:i + batch_size]).cpu().numpy())
+        return np.concatenate(outs, axis=0) if outs else np.zeros((0, L.MAX_DETECT, 6),
+                                                                  np.float32)
+
+    def count_params(self) -> int:
+        return int(sum(int(np.prod(s)) for s in self.weight_shapes.values()))
+
+
+_DEFAULTS = dict(                                          # vtd.py:498-506
+    input_shape=None, patch_size=17, embedding_dim=28, encoder_num_heads=8,
+    encoder_key_dim=40, dropout=None, encoder_mlp_quantities=8, encoder_repeat_times=8,
+    mlp_head_last_units=136, mlp_head_dense_layers_quantity=7,
+    mlp_head_dense_mish_block_repeats=1, use_mish=True, max_weight=10, clip_weight=True,
+    training=None)
+
+
+def create_vision_transformer_detector(
+        input_shape=None, patch_size=17, embedding_dim=28,
+        encoder_num_heads=8, encoder_key_dim=40, dropout=None,
+        encoder_mlp_quantities=8,
+        encoder_repeat_times=8,
+        mlp_head_last_units=136, mlp_head_dense_layers_quantity=7,
+        mlp_head_dense_mish_block_repeats=1,
+        use_mish=True,
+        max_weight=10, clip_weight=True, training=None,
+        *, dtype="bfloat16", device=None, seed=0) -> Model:
+    """Same kwargs and defaults as vtd.py:498-506.  `dropout` must be None or 0 (the
+    forward path is inference-only); `max_weight`/`clip_weight` are weight constraints
+    Keras applies only after optimizer steps (vtd.py:209-236), so they do not affect
+    the forward and are accepted as no-ops.  Extra keyword-only options: `dtype`
+    ('bfloat16' throughput mode or 'float32' parity mode), `device`, `seed`."""
+    if dropout not in (None, 0, 0.0):
+        raise ValueError("dropout must be None or 0 for the inference forward path")
+    if input_shape is None:                                       # vtd.py:550-551
+        input_shape = (*Constants.MODEL_IMAGE_SIZE.value, 3)
+    kw = dict(input_shape=tuple(int(v) for v in input_shape), patch_size=int(patch_size),
+              embedding_dim=int(embedding_dim), encoder_num_heads=int(encoder_num_heads),
+              encoder_key_dim=int(encoder_key_dim), dropout=dropout,
+              encoder_mlp_quantities=int(encoder_mlp_quantities),
+              encoder_repeat_times=int(encoder_repeat_times),
+              mlp_head_last_units=int(mlp_head_last_units),
+              mlp_head_dense_layers_quantity=int(mlp_head_dense_layers_quantity),
+              mlp_head_dense_mish_block_repeats=int(mlp_head_dense_mish_block_repeats),
+              use_mish=bool(use_mish), max_weight=max_weight, clip_weight=clip_weight,
+              training=training)
+    return Model(kw, dtype=dtype, device=device, seed=seed)
+
+
+def transform_predictions(inputs):
+    """vtd.py:586-647 on a (…, 6) tensor/array: sigmoid; clip the last 4 to [0, 1];
+    [objectness, class * (CLASSES - 1), cx * W, cy * H, h * H, w * W] with (H, W) the
+    constant MODEL_IMAGE_SIZE = (608, 608).  Device tensors decode on the GPU via
+    vtd_decode; numpy/CPU inputs are rejected (no CPU path)."""
+    t = inputs if torch.is_tensor(inputs) else torch.as_tensor(np.asarray(inputs))
+    if t.device.type != "cuda":
+        raise ValueError("transform_predictions runs on the HIP device: pass a cuda tensor")
+    if t.shape[-1] != 6:
+        raise ValueError(f"expected last dim 6, got {tuple(t.shape)}")
+    src = t.to(torch.float32).contiguous()
+    out = torch.empty_like(src)
+    n = src.numel() // 6
+    if n:
+        with torch.cuda.device(src.device):
+            L.check(L.lib.vtd_decode(src.data_ptr(), n, out.data_ptr(), L.stream_ptr()),
+                    "vtd_decode")
+    return out
