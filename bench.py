@@ -1,0 +1,212 @@
+"""Headline benchmark: images/s of the ViT-B/16 detector forward at batch 256 per GPU
+(BASELINE.json metric), bf16 operands / fp32 accumulate, synthetic COCO-shaped batches.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--dtype bf16|f32]
+  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+One step = one forward of B images per rank (images already resident in HBM) + the
+device-side decode (transform_predictions) + the RCCL all-gather of the (B, 17, 6)
+detections over all ranks (the path's only exchange; skipped at N = 1).
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_TFLOPS = {"bf16": 2516.6, "f32": 157.3}   # MI355X dense: 256 CU x 2.4 GHz (MICROARCH)
+HBM_PEAK_GBS = 8000.0
+
+
+def letterbox_images(b, shape, gen, device):
+    """U(-1, 1) NHWC images with -1 letterbox bands: a 640x480 COCO image resized with
+    pad to a square (utils.py:438-447) keeps 3/4 of the rows."""
+    h, w, c = shape
+    x = torch.rand((b, h, w, c), generator=gen, device=device) * 2 - 1
+    band = h // 8
+    x[:, :band] = -1.0
+    x[:, h - band:] = -1.0
+    return x
+
+
+def algorithmic_flops_per_image(kw, dims):
+    """2 x MAC over every Dense / attention product as written in the reference
+    (no padding), SURVEY.md §8d.  Returns (total, attention+MLP)."""
+    n, d = dims.tokens, kw["embedding_dim"]
+    h, dk = kw["encoder_num_heads"], kw["encoder_key_dim"]
+    inner = h * dk
+    patch = 2.0 * n * dims.patch_dim * d
+    qkv = 2.0 * n * d * 3 * inner
+    attn = 4.0 * h * n * n * dk
+    out = 2.0 * n * inner * d
+    mlp, k = 0.0, d
+    for j in range(kw["encoder_mlp_quantities"]):
+        mlp += 2.0 * n * k * dims.mlp_units[j]
+        k = dims.mlp_units[j]
+    L = kw["encoder_repeat_times"]
+    head = 2.0 * n * d * 17
+    k = n
+    for j in range(dims.n_head):
+        head += 2.0 * 17 * k * dims.head_units[j]
+        k = dims.head_units[j]
+    head += 2.0 * 17 * k * 6
+    total = patch + L * (qkv + attn + out + mlp) + head
+    return total, L * (qkv + attn + out + mlp)
+
+
+def cpu_baseline(model, kw, shape, seconds=12.0):
+    """The oracle's fp32 torch-CPU restatement (oracle/vtd_torch_cpu.py) of the same
+    graph on the host cores: the reference's TF-CPU path cannot run in this pipeline
+    (TF/Keras/tfa absent), so this is the "port" baseline."""
+    from oracle.vtd_torch_cpu import TorchCpuDetector
+    threads = torch.get_num_threads()
+    det = TorchCpuDetector(model.get_weight_dict(), **kw)
+    b = 4
+    x = letterbox_images(b, shape, torch.Generator().manual_seed(7), "cpu")
+    det(x)                                   # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        det(x)
+        n += 1
+        el = time.perf_counter() - t0
+        if el > seconds or n >= 50:
+            break
+    return {"value": b * n / el, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} forwards x batch {b} ({b * n} images, {el:.1f} s) of the same "
+                      f"preset on the fp32 torch-CPU restatement, {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--preset", default="vit_b16_224")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import vision_transformer_detector_amd as vtd
+    from vision_transformer_detector_amd import _lib as L
+    kw = dict(vtd.presets.PRESETS[args.preset])
+    # identical weights on every rank (same seed): replicated-weight data parallelism
+    model = vtd.create_vision_transformer_detector(
+        **kw, dtype="bfloat16" if args.dtype == "bf16" else "float32", device=dev, seed=0)
+    kw = {k: model.kwargs[k] for k in model.kwargs}
+    shape = model.input_shape
+    B = args.batch
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    images = letterbox_images(B, shape, gen, dev)
+    gathered = torch.empty((world * B, 17, 6), dtype=torch.float32, device=dev)
+
+    def step():
+        logits, dets = model.detect(images)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, dets)
+        return logits
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---- per-kernel timing: hipEvents recorded around every launch of vtd_forward on
+    # the stream it launches on, over K more steps of the same workload
+    L.check(L.lib.vtd_profile_reset())
+    L.check(L.lib.vtd_profile_enable(1))
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    prof_elapsed = time.perf_counter() - t1
+    L.check(L.lib.vtd_profile_enable(0))
+    import ctypes
+    ms = (ctypes.c_double * L.PROF_CLASSES)()
+    nl = (ctypes.c_int64 * L.PROF_CLASSES)()
+    fl = (ctypes.c_double * L.PROF_CLASSES)()
+    L.check(L.lib.vtd_profile_read(ms, nl, fl, L.PROF_CLASSES))
+    classes = ["gemm", "attention", "layernorm", "patches", "other"]
+    kernels = {c: {"ms_total": ms[i], "launches": int(nl[i]),
+                   "avg_us": 1e3 * ms[i] / max(1, nl[i]),
+                   "tflops": (fl[i] / (ms[i] * 1e-3) / 1e12) if ms[i] > 0 and fl[i] > 0 else None}
+               for i, c in enumerate(classes)}
+
+    total_fl, attn_mlp_fl = algorithmic_flops_per_image(kw, model.dims)
+    ms_per_step = 1e3 * elapsed / args.steps
+    img_s = world * B * args.steps / elapsed
+    peak = PEAK_TFLOPS[args.dtype]
+    g = kernels["gemm"]
+    gemm_tf = g["tflops"]
+    out = {
+        "metric": "images/sec ViT-B/16 detector fwd, batch 256, 1/2/4/8 MI355X; MFMA util %",
+        "value": round(img_s, 2),
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (U(-1,1) NHWC letterboxed images generated on device; "
+                "random Keras-default-init weights)",
+        "config": {"workload": f"{args.preset} detector forward + decode + all-gather of "
+                               f"detections", "per_gpu_batch": B, "global_batch": world * B,
+                   "input_shape": list(shape), "tokens": model.dims.tokens,
+                   "parallelism": f"dp{world}"},
+        "mfma_util_attn_mlp": round(attn_mlp_fl * img_s / world / (peak * 1e12), 4),
+        "model_tflops_per_gpu": round(total_fl * img_s / world / 1e12, 1),
+        "roofline": {"bound": "mfma", "kernel": "gemm_tn_kernel (all Dense layers)",
+                     "achieved": round(gemm_tf, 1) if gemm_tf else None, "peak": peak,
+                     "unit": "TFLOP/s",
+                     "frac": round(gemm_tf / peak, 4) if gemm_tf else None,
+                     "traffic": None,
+                     "avg_launch_us": round(g["avg_us"], 2),
+                     "launches_per_step": g["launches"] // max(1, args.steps)},
+        "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv)
+                        for kk, vv in v.items()} for k, v in kernels.items()},
+        "profiled_ms_per_step": round(1e3 * prof_elapsed / args.steps, 3),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(model, kw, shape, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -145,9 +145,9 @@ def test_layernorm(L, cuda, dtype, D, ld):
     gamma = torch.zeros(ld); gamma[:D] = 1 + 0.1 * torch.randn(D, generator=g)
     beta = torch.zeros(ld); beta[:D] = 0.1 * torch.randn(D, generator=g)
     y = torch.full((rows, ld), float("nan"), dtype=tdt, device=cuda)
-    L.check(L.lib.vtd_layernorm(x.to(cuda).data_ptr(), rows, D, ld, gamma.to(cuda).data_ptr(),
-                                beta.to(cuda).data_ptr(), 1e-3, y.data_ptr(), ld, code,
-                                L.stream_ptr()), "ln")
+    xd, gd, bd = x.to(cuda), gamma.to(cuda), beta.to(cuda)   # keep device copies alive
+    L.check(L.lib.vtd_layernorm(xd.data_ptr(), rows, D, ld, gd.data_ptr(), bd.data_ptr(),
+                                1e-3, y.data_ptr(), ld, code, L.stream_ptr()), "ln")
     torch.cuda.synchronize()
     exp = ref.layer_norm(x[:, :D].double().numpy(), gamma[:D].double().numpy(),
                          beta[:D].double().numpy())
@@ -163,7 +163,8 @@ def test_layernorm_epsilon_kat(L, cuda):
     x = torch.tensor([(-1) ** i * math.sqrt(1e-3) for i in range(D)], dtype=torch.float32)
     y = torch.zeros(1, D, device=cuda)
     one, zero = torch.ones(D, device=cuda), torch.zeros(D, device=cuda)
-    L.check(L.lib.vtd_layernorm(x.to(cuda).data_ptr(), 1, D, D, one.data_ptr(),
+    xd = x.to(cuda)
+    L.check(L.lib.vtd_layernorm(xd.data_ptr(), 1, D, D, one.data_ptr(),
                                 zero.data_ptr(), 1e-3, y.data_ptr(), D, L.F32, L.stream_ptr()))
     torch.cuda.synchronize()
     assert abs(y[0, 0].item() - math.sqrt(1e-3) / math.sqrt(2e-3)) < 1e-5
@@ -194,7 +195,8 @@ def test_attention(L, cuda, dtype, B, N, H, dk):
     qkv_t = torch.from_numpy(qkv).to(tdt)
     ldo = H * dkp
     out = torch.full((B * N, ldo), float("nan"), dtype=tdt, device=cuda)
-    L.check(L.lib.vtd_attention(qkv_t.to(cuda).data_ptr(), B, N, H, dkp, ld,
+    qkv_d = qkv_t.to(cuda)
+    L.check(L.lib.vtd_attention(qkv_d.data_ptr(), B, N, H, dkp, ld,
                                 1.0 / math.sqrt(dk), out.data_ptr(), ldo, code,
                                 L.stream_ptr()), "attention")
     torch.cuda.synchronize()
@@ -213,7 +215,8 @@ def test_attention_uniform_kat(L, cuda):
     qkv = torch.zeros(B * N, 3 * H * dkp)
     qkv[:, H * dkp:] = torch.randn(B * N, 2 * H * dkp, generator=g)
     out = torch.zeros(B * N, H * dkp, device=cuda)
-    L.check(L.lib.vtd_attention(qkv.to(cuda).data_ptr(), B, N, H, dkp, 3 * H * dkp, 0.125,
+    qkv_d = qkv.to(cuda)
+    L.check(L.lib.vtd_attention(qkv_d.data_ptr(), B, N, H, dkp, 3 * H * dkp, 0.125,
                                 out.data_ptr(), H * dkp, L.F32, L.stream_ptr()))
     torch.cuda.synchronize()
     v = qkv[:, 2 * H * dkp:].double()
@@ -231,7 +234,8 @@ def test_extract_patches(L, cuda, dtype, H, W, p):
     P = p * p * C
     ld = ((P + 63) // 64) * 64
     out = torch.full((B * exp.shape[1], ld), float("nan"), dtype=tdt, device=cuda)
-    L.check(L.lib.vtd_extract_patches(torch.from_numpy(img).to(cuda).data_ptr(), B, H, W, C,
+    img_d = torch.from_numpy(img).to(cuda)
+    L.check(L.lib.vtd_extract_patches(img_d.data_ptr(), B, H, W, C,
                                       p, out.data_ptr(), ld, code, L.stream_ptr()))
     torch.cuda.synchronize()
     got = out.cpu()
@@ -245,7 +249,8 @@ def test_decode_matches_oracle(L, cuda):
     logits = g.normal(0, 4, size=(5, 17, 6)).astype(np.float32)
     logits[0, 0] = 0.0
     dets = torch.zeros(5, 17, 6, device=cuda)
-    L.check(L.lib.vtd_decode(torch.from_numpy(logits).to(cuda).data_ptr(), 5 * 17,
+    logits_d = torch.from_numpy(logits).to(cuda)
+    L.check(L.lib.vtd_decode(logits_d.data_ptr(), 5 * 17,
                              dets.data_ptr(), L.stream_ptr()))
     torch.cuda.synchronize()
     exp = ref.transform_predictions(logits)
