@@ -265,3 +265,28 @@ def test_bad_args_raise_value_error(L, cuda):
     with pytest.raises(ValueError):
         L.check(L.lib.vtd_gemm(16, 16, 30, 1, 32, 1, 32, L.BF16, ctypes.byref(e),
                                L.stream_ptr()), "gemm")
+
+
+@pytest.mark.parametrize("M,N,K,act,out_dtype", [
+    (4100, 2100, 192, 0, 0), (4100, 2100, 192, 1, 1), (8192, 1024, 64, 2, 0),
+    (3000, 3000, 320, 1, 1), (4352, 8704, 256, 1, 1)])
+def test_gemm_bf16_256_tile_path(L, cuda, M, N, K, act, out_dtype):
+    """Large problems (>= 128 tiles of 256 x 256) take the DMA-staged 256-tile kernel;
+    ragged M / N exercise the clamped loads and masked epilogue."""
+    g = torch.Generator(device=cuda).manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
+    Bt = (torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g, device=cuda)
+    resid = torch.randn(M, N, generator=g, device=cuda) if out_dtype == 0 else None
+    out = torch.full((M, N), float("nan"), device=cuda,
+                     dtype=torch.float32 if out_dtype == 0 else torch.bfloat16)
+    _gemm(L, A, Bt, L.BF16, bias=bias, act=act, resid=resid, out=out, out_dtype=out_dtype)
+    ref64 = (A.double() @ Bt.double().T + bias.double()).cpu().numpy()
+    ref64 = _np_act(act, ref64)
+    if resid is not None:
+        ref64 = ref64 + resid.double().cpu().numpy()
+    got = out.double().cpu().numpy()
+    tol = 2e-5 if out_dtype == 0 else 8e-3
+    err = np.abs(got - ref64) / np.maximum(np.abs(ref64), 1.0)
+    bad = np.argwhere(err >= tol)
+    assert err.max() < tol, (err.max(), len(bad), bad[:5].tolist())

@@ -79,6 +79,46 @@ __device__ __forceinline__ void swrite4(const i32x4 (&ra)[4], const i32x4 (&rb)[
   }
 }
 
+// Four consecutive columns n..n+3 of row m (row-vector epilogue of the staged path).
+__device__ __forceinline__ void epi_store4(const EpiArgs& e, int M, int N, int m, int n,
+                                           f32x4 v) {
+  if (m >= M) return;
+  const bool full = (n + 3 < N) && e.scatter_tokens <= 0 && (e.ldo & 3) == 0 &&
+                    (!e.resid || (e.ldr & 3) == 0) && (!e.out2 || (e.ldo2 & 3) == 0);
+  if (!full) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) epi_store(e, M, N, m, n + j, v[j]);
+    return;
+  }
+  if (e.bias) {
+    const f32x4 b = *reinterpret_cast<const f32x4*>(e.bias + n);
+    v += b;
+  }
+  if (e.rowadd) {
+    const float ra = e.rowadd[m % e.rowadd_period];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] += (n + j < e.rowadd_ncols) ? ra : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = apply_act(e.act, v[j]);
+  if (e.resid) v += *reinterpret_cast<const f32x4*>(e.resid + (int64_t)m * e.ldr + n);
+  const int64_t idx = (int64_t)m * e.ldo + n;
+  if (e.out_dtype == VTD_F32) {
+    *reinterpret_cast<f32x4*>(static_cast<float*>(e.out) + idx) = v;
+  } else {
+    bf16x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = static_cast<short>(f32_to_bf16(v[j]));
+    *reinterpret_cast<bf16x4*>(static_cast<bf16_t*>(e.out) + idx) = o;
+  }
+  if (e.out2) {
+    bf16x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = static_cast<short>(f32_to_bf16(v[j]));
+    *reinterpret_cast<bf16x4*>(static_cast<bf16_t*>(e.out2) + (int64_t)m * e.ldo2 + n) = o;
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(NT) void gemm_tn_kernel(
     int M, int N, int K, const T* __restrict__ A, int lda, const T* __restrict__ Bt,
@@ -167,6 +207,136 @@ __global__ __launch_bounds__(NT) void gemm_tn_kernel(
       }
 }
 
+// ============================================================================
+// bf16 "big" kernel: 256 x 256 tile, BK = 64, 512 threads = 8 waves (2 M x 4 N), each
+// wave 128 x 64 outputs = 8 x 4 blocks of v_mfma_f32_16x16x32_bf16.
+// Operands go HBM/L2 -> LDS directly with global_load_lds_dwordx4 (no VGPR staging):
+// one wave-instruction writes 1 KiB = 8 rows of 128 B, lane-linear in LDS; the
+// chunk ^= row & 7 swizzle is applied on the per-lane GLOBAL source address and again
+// on the ds_read, so the LDS image is the same as the 128-tile kernel's.
+// Two LDS stages of 64 KiB (A 32 KiB + B 32 KiB).  Tile t+1's DMA stays in flight while
+// tile t is computed: counted `s_waitcnt vmcnt(8)` (8 DMA instructions per wave per
+// tile) + raw s_barrier, never __syncthreads() (its fence would drain the DMA).
+// Tiles are remapped so consecutive tiles (sharing an A panel) run on one XCD (T1).
+// ============================================================================
+constexpr int BBM = 256, BBN = 256, BNT = 512;
+constexpr int BSTAGE = (BBM + BBN) * KB;     // 64 KiB per stage
+static_assert(8 * 32 * 68 * 4 <= 2 * BSTAGE, "epilogue staging must fit the stages");
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+__device__ __forceinline__ void glds16(const char* g, char* lds_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)lds_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ void issue_tile(char* smem, const char* const (&srcA)[4],
+                                           const char* const (&srcB)[4], int lds_piece,
+                                           int kt, int stage) {
+  char* base = smem + stage * BSTAGE;
+  const int64_t ko = (int64_t)kt * KB;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) glds16(srcA[j] + ko, base + lds_piece + j * 8 * KB);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) glds16(srcB[j] + ko, base + BBM * KB + lds_piece + j * 8 * KB);
+}
+
+__global__ __launch_bounds__(BNT) void gemm_tn_bf16_256_kernel(
+    int M, int N, int K, const bf16_t* __restrict__ A, int lda,
+    const bf16_t* __restrict__ Bt, int ldb, int tiles_m, int tiles_n, EpiArgs e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // ---- XCD-aware bijective tile remap: blocks b, b+8, ... share an XCD
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tm = tile / tiles_n, tn = tile - (tile / tiles_n) * tiles_n;
+  const int m0 = tm * BBM, n0 = tn * BBN;
+
+  // ---- DMA source addresses: this wave fills rows [wave*32, wave*32+32) of the A tile
+  // and of the B tile, as 4 pieces of 8 rows; lane l -> row +(l>>3), logical chunk
+  // (l & 7) ^ (l >> 3) (the row's swizzle), so the LDS image is row*128 + (c^(row&7))*16.
+  const int prow = lane >> 3;
+  const int pchunk = (lane & 7) ^ prow;
+  const char* srcA[4];
+  const char* srcB[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = wave * 32 + j * 8 + prow;
+    srcA[j] = reinterpret_cast<const char*>(A + (int64_t)min(m0 + row, M - 1) * lda) + pchunk * 16;
+    srcB[j] = reinterpret_cast<const char*>(Bt + (int64_t)min(n0 + row, N - 1) * ldb) + pchunk * 16;
+  }
+  const int lds_piece = wave * 32 * KB;       // byte offset of this wave's first piece
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fg = lane >> 4;
+  const int nk = K / 64;
+  issue_tile(smem, srcA, srcB, lds_piece, 0, 0);
+  if (nk > 1) issue_tile(smem, srcA, srcB, lds_piece, 1, 1);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const char* la = smem + (kt & 1) * BSTAGE;
+    const char* lb = la + BBM * KB;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = 4 * s + fg;
+      bf16x8 af[8], bfr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8*>(lb + swz(wn * 64 + j * 16 + fr, c));
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(la + swz(wm * 128 + i * 16 + fr, c));
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 2 < nk) issue_tile(smem, srcA, srcB, lds_piece, kt + 2, kt & 1);
+  }
+
+  // ---- epilogue staged through LDS (the stages are free after the last barrier):
+  // each wave owns a private 32 x 68-float region (8 waves x 8.5 KiB); pass p stages
+  // accumulator rows i = 2p, 2p+1 (32 rows x 64 cols), then reads them back as row
+  // vectors so bias / activation / residual / store use 16-B coalesced accesses.
+  constexpr int ES = 68;      // row stride (floats): rows 4 apart hit opposite bank halves
+  float* ep = reinterpret_cast<float*>(smem) + wave * 32 * ES;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r2 = 0; r2 < 4; ++r2)
+          ep[(i * 16 + fg * 4 + r2) * ES + j * 16 + fr] = acc[p * 2 + i][j][r2];
+#pragma unroll 4
+    for (int it = 0; it < 8; ++it) {
+      const int row = it * 4 + (lane >> 4), col = (lane & 15) * 4;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(ep + row * ES + col);
+      epi_store4(e, M, N, m0 + wm * 128 + p * 32 + row, n0 + wn * 64 + col, v);
+    }
+  }
+}
+
 }  // namespace
 
 int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
@@ -189,7 +359,18 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM);
   const size_t lds = 4 * TILE_BYTES;
   ProfScope ps(stream, PROF_GEMM, flops > 0 ? flops : 2.0 * M * N * (double)K);
-  if (dtype == VTD_BF16)
+  const int tiles_m = (M + BBM - 1) / BBM, tiles_n = (N + BBN - 1) / BBN;
+  if (dtype == VTD_BF16 && tiles_m * tiles_n >= 128) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_bf16_256_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
+      attr = true;
+    }
+    hipLaunchKernelGGL(gemm_tn_bf16_256_kernel, dim3(tiles_m * tiles_n), dim3(BNT),
+                       2 * BSTAGE, stream, M, N, K, static_cast<const bf16_t*>(A), lda,
+                       static_cast<const bf16_t*>(Bt), ldb, tiles_m, tiles_n, e);
+  } else if (dtype == VTD_BF16)
     hipLaunchKernelGGL(gemm_tn_kernel<bf16_t>, grid, dim3(NT), lds, stream, M, N, K,
                        static_cast<const bf16_t*>(A), lda,
                        static_cast<const bf16_t*>(Bt), ldb, e);
