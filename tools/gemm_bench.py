@@ -1,0 +1,83 @@
+"""GEMM micro-benchmark through the C-ABI: TFLOP/s per encoder shape (C2, B=256) and a
+square reference shape, for A/B-ing kernel variants (VTD_GEMM_VARIANT) in one process.
+
+  python tools/gemm_bench.py [--variants 0,1] [--reps 20]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vision_transformer_detector_amd import _lib as L  # noqa: E402
+
+SHAPES = {  # name: (M, N, K, act, out_dtype, resid)
+    "qkv": (50176, 2304, 768, 0, 1, False),
+    "attn_out": (50176, 768, 768, 0, 0, True),
+    "mlp1": (50176, 3072, 768, 1, 1, False),
+    "mlp2": (50176, 1536, 3072, 1, 1, False),
+    "mlp3": (50176, 768, 1536, 1, 0, True),
+    "head1": (4352, 8704, 256, 1, 1, False),
+    "head2": (4352, 4352, 8704, 1, 1, False),
+    "sq8192": (8192, 8192, 8192, 0, 1, False),
+}
+
+
+def run(name, spec, reps, dev):
+    M, N, K, act, od, res = spec
+    g = torch.Generator(device=dev).manual_seed(0)
+    A = (torch.rand(M, K, generator=g, device=dev) * 2 - 1).to(torch.bfloat16)
+    Bt = (torch.rand(N, K, generator=g, device=dev) * 2 - 1).to(torch.bfloat16)
+    bias = torch.zeros(N, device=dev)
+    out = torch.empty(M, N, device=dev, dtype=torch.float32 if od == 0 else torch.bfloat16)
+    e = L.VtdEpilogue()
+    e.bias = bias.data_ptr()
+    e.act = act
+    e.out, e.ldo, e.out_dtype = out.data_ptr(), N, od
+    if res:
+        e.resid, e.ldr = out.data_ptr(), N
+    st = L.stream_ptr()
+    call = lambda: L.check(L.lib.vtd_gemm(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K,
+                                          L.BF16, ctypes.byref(e), st))
+    for _ in range(3):
+        call()
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0.record()
+    for _ in range(reps):
+        call()
+    t1.record()
+    torch.cuda.synchronize()
+    ms = t0.elapsed_time(t1) / reps
+    res = {"shape": name, "us": round(ms * 1e3, 1), "tflops": round(2 * M * N * K / ms / 1e9, 1)}
+    if os.environ.get("VTD_GEMM_REF_LIB"):
+        # vendor-library reference (torch.matmul -> hipBLASLt), timing comparison only
+        Bk = Bt.t()
+        o = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        for _ in range(3):
+            torch.matmul(A, Bk, out=o)
+        t0.record()
+        for _ in range(reps):
+            torch.matmul(A, Bk, out=o)
+        t1.record()
+        torch.cuda.synchronize()
+        ms2 = t0.elapsed_time(t1) / reps
+        res["vendor_lib_tflops"] = round(2 * M * N * K / ms2 / 1e9, 1)
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--shapes", default=",".join(SHAPES))
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    for name in args.shapes.split(","):
+        print(json.dumps({"variant": os.environ.get("VTD_GEMM_VARIANT", "default"),
+                          **run(name, SHAPES[name], args.reps, dev)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -11,6 +11,8 @@
 // (written after them), two LDS buffers, one barrier per K step.  LDS rows are 128 B and
 // XOR-swizzled on the 16-B chunk index (chunk ^= row & 7) so the 16 rows read by one
 // ds_read_b128 lane group spread over the banks.
+#include <stdlib.h>
+
 #include "vtd_common.h"
 
 namespace vtd {
@@ -337,6 +339,290 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_256_kernel(
   }
 }
 
+
+// ============================================================================
+// bf16 "ping-pong" kernel: same tile (256 x 256, BK 64), LDS image, DMA staging and
+// epilogue as gemm_tn_bf16_256_kernel, but the 8 waves run as two groups offset by one
+// barrier: G0 = waves 0-3 (A rows 0-127), G1 = waves 4-7 (A rows 128-255).  Each SIMD
+// holds one wave of each group, so while one group issues its MFMAs the other issues
+// its LDS reads and DMA (the two pipes overlap instead of alternating).
+//
+// A K-tile is 4 phases; a phase = [L: ds_reads (+ DMA)] barrier [C: 16 MFMAs] barrier,
+// computing one 64 x 32 quadrant of the wave's 128 x 64 tile:
+//   P0: a <- A quad 0, b0 <- B quad 0, DMA A of tile t+1 | C: acc[0..3][0..1]
+//   P1: b1 <- B quad 1, DMA B of tile t+1                | C: acc[0..3][2..3]
+//   P2: a <- A quad 1                                    | C: acc[4..7][2..3]
+//   P3: s_waitcnt vmcnt(0) (tile t+1 landed)             | C: acc[4..7][0..1]
+// Barrier bookkeeping (event e = e-th workgroup barrier; G1 runs one extra barrier
+// first, G0 one extra last): G0's L_p ends at event 2p+1, G1's at 2p+2.  Hazards:
+//   RAW (DMA -> ds_read): every wave drains its DMA (vmcnt(0)) in L_{4t+3}, before
+//     event 8t+8; the first read of tile t+1 (G0, L_{4t+4}) starts after event 8t+8.
+//   WAR (ds_read -> DMA into the same stage): the last reads of tile t-1 (L_{4t-2},
+//     retired by the lgkmcnt wait in C_{4t-2}) finish before event 8t-1; the DMA of
+//     tile t+1 into that stage issues in L_{4t}, after event 8t.
+// ============================================================================
+// ---- specialized epilogue (EPI = act | out_bf16 << 2 | resid << 3), full tiles only
+constexpr int EPI_GENERIC = -1;
+__host__ __device__ constexpr int epi_code(int act, bool out_bf16, bool resid) {
+  return act | (out_bf16 ? 4 : 0) | (resid ? 8 : 0);
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_ct(float x) {
+  if constexpr (ACT == VTD_ACT_GELU_TANH) return act_gelu(x);
+  else if constexpr (ACT == VTD_ACT_MISH) return act_mish(x);
+  else return x;
+}
+
+// Writes the wave's 128 x 64 accumulator tile: 4 passes of 32 rows staged through the
+// wave's private LDS region; each lane then owns 8 consecutive columns of a row, so
+// residual reads and output writes are 16-B per lane (one 128-B line per 8 lanes).
+template <int EPI, bool kDiagNoStore = false>
+__device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* ep, int lane,
+                                              int m_base, int n_base, const EpiArgs& e) {
+  constexpr int ACT = EPI & 3;
+  constexpr bool OUT_BF16 = (EPI & 4) != 0;
+  constexpr bool RESID = (EPI & 8) != 0;
+  constexpr int ES = 68;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int c8 = (lane & 7) * 8, rsub = lane >> 3;
+  const f32x4 b0 = *reinterpret_cast<const f32x4*>(e.bias + n_base + c8);
+  const f32x4 b1 = *reinterpret_cast<const f32x4*>(e.bias + n_base + c8 + 4);
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r2 = 0; r2 < 4; ++r2)
+          ep[(i * 16 + fg * 4 + r2) * ES + j * 16 + fr] = acc[p * 2 + i][j][r2];
+    f32x4 rv[4][2];
+    if constexpr (RESID) {
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int64_t m = m_base + p * 32 + it * 8 + rsub;
+        const float* rp = e.resid + m * e.ldr + n_base + c8;
+        rv[it][0] = *reinterpret_cast<const f32x4*>(rp);
+        rv[it][1] = *reinterpret_cast<const f32x4*>(rp + 4);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int row = it * 8 + rsub;
+      f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + row * ES + c8) + b0;
+      f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + row * ES + c8 + 4) + b1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v0[j] = act_ct<ACT>(v0[j]);
+        v1[j] = act_ct<ACT>(v1[j]);
+      }
+      if constexpr (RESID) {
+        v0 += rv[it][0];
+        v1 += rv[it][1];
+      }
+      const int64_t idx = (int64_t)(m_base + p * 32 + row) * e.ldo + n_base + c8;
+      if constexpr (kDiagNoStore) {
+        if (v0[0] != v0[0] && v1[3] != v1[3]) static_cast<float*>(e.out)[idx] = v0[1];
+      } else if constexpr (OUT_BF16) {
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          o[j] = static_cast<short>(f32_to_bf16(v0[j]));
+          o[j + 4] = static_cast<short>(f32_to_bf16(v1[j]));
+        }
+        *reinterpret_cast<bf16x8*>(static_cast<bf16_t*>(e.out) + idx) = o;
+      } else {
+        float* op = static_cast<float*>(e.out) + idx;
+        *reinterpret_cast<f32x4*>(op) = v0;
+        *reinterpret_cast<f32x4*>(op + 4) = v1;
+      }
+    }
+  }
+}
+
+// Runtime-flag epilogue for partial tiles and rare modes (rowadd, scatter, out2): the
+// accumulators are staged into LDS inline (static register indices), and only the
+// LDS -> global loop is kept rolled (keeps the kernel small).
+__device__ __forceinline__ void epilogue_generic_pass(const float* ep, int lane, int M, int N,
+                                                   int m_base, int n_base, const EpiArgs& e) {
+  constexpr int ES = 68;
+#pragma unroll 1
+  for (int it = 0; it < 8; ++it) {
+    const int row = it * 4 + (lane >> 4), col = (lane & 15) * 4;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(ep + row * ES + col);
+    epi_store4(e, M, N, m_base + row, n_base + col, v);
+  }
+}
+
+__device__ __forceinline__ void epilogue_generic(const f32x4 (&acc)[8][4], float* ep, int lane,
+                                                 int M, int N, int m_base, int n_base,
+                                                 const EpiArgs& e) {
+  constexpr int ES = 68;
+  const int fr = lane & 15, fg = lane >> 4;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r2 = 0; r2 < 4; ++r2)
+          ep[(i * 16 + fg * 4 + r2) * ES + j * 16 + fr] = acc[p * 2 + i][j][r2];
+    epilogue_generic_pass(ep, lane, M, N, m_base + p * 32, n_base, e);
+  }
+}
+
+__device__ __forceinline__ void pp_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int I0, int J0>
+__device__ __forceinline__ void pp_mfma(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][2],
+                                        const bf16x8 (&b)[2][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[I0 + i][J0 + j] =
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s], b[j][s], acc[I0 + i][J0 + j], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+__device__ __forceinline__ void pp_load_a(bf16x8 (&a)[4][2], const char* la, int row0, int fr,
+                                          int fg) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      a[i][s] = *reinterpret_cast<const bf16x8*>(la + swz(row0 + i * 16 + fr, 4 * s + fg));
+}
+__device__ __forceinline__ void pp_load_b(bf16x8 (&b)[2][2], const char* lb, int row0, int fr,
+                                          int fg) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      b[j][s] = *reinterpret_cast<const bf16x8*>(lb + swz(row0 + j * 16 + fr, 4 * s + fg));
+}
+
+template <int EPI, bool kDiagSkipEpilogue>
+__global__ __launch_bounds__(BNT) void gemm_tn_bf16_pingpong_kernel(
+    int M, int N, int K, const bf16_t* __restrict__ A, int lda,
+    const bf16_t* __restrict__ Bt, int ldb, int tiles_m, int tiles_n, EpiArgs e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tm = tile / tiles_n, tn = tile - (tile / tiles_n) * tiles_n;
+  const int m0 = tm * BBM, n0 = tn * BBN;
+
+  const int prow = lane >> 3;
+  const int pchunk = (lane & 7) ^ prow;
+  const char* srcA[4];
+  const char* srcB[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = wave * 32 + j * 8 + prow;
+    srcA[j] = reinterpret_cast<const char*>(A + (int64_t)min(m0 + row, M - 1) * lda) + pchunk * 16;
+    srcB[j] = reinterpret_cast<const char*>(Bt + (int64_t)min(n0 + row, N - 1) * ldb) + pchunk * 16;
+  }
+  const int lds_piece = wave * 32 * KB;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fg = lane >> 4;
+  const int nk = K / 64;
+  const int arow = wm * 128, brow = wn * 64;
+
+  // prologue: tile 0 -> stage 0, visible to all waves
+  issue_tile(smem, srcA, srcB, lds_piece, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  pp_barrier();
+  if (wm == 1) pp_barrier();                 // stagger G1 by one barrier
+
+  bf16x8 a[4][2], b0[2][2], b1[2][2];
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* la = smem + (kt & 1) * BSTAGE;
+    const char* lb = la + BBM * KB;
+    char* nxt = smem + ((kt + 1) & 1) * BSTAGE;
+    const bool pf = kt + 1 < nk;
+    const int64_t ko = (int64_t)(kt + 1) * KB;
+    // ---- P0
+    pp_load_a(a, la, arow, fr, fg);
+    pp_load_b(b0, lb, brow, fr, fg);
+    if (pf) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) glds16(srcA[j] + ko, nxt + lds_piece + j * 8 * KB);
+    }
+    pp_barrier();
+    pp_mfma<0, 0>(acc, a, b0);
+    pp_barrier();
+    // ---- P1
+    pp_load_b(b1, lb, brow + 32, fr, fg);
+    if (pf) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        glds16(srcB[j] + ko, nxt + BBM * KB + lds_piece + j * 8 * KB);
+    }
+    pp_barrier();
+    pp_mfma<0, 2>(acc, a, b1);
+    pp_barrier();
+    // ---- P2
+    pp_load_a(a, la, arow + 64, fr, fg);
+    pp_barrier();
+    pp_mfma<4, 2>(acc, a, b1);
+    pp_barrier();
+    // ---- P3
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pp_barrier();
+    pp_mfma<4, 0>(acc, a, b0);
+    pp_barrier();
+  }
+  if (wm == 0) pp_barrier();                 // re-align: every wave past its last section
+
+  if constexpr (kDiagSkipEpilogue && EPI >= 0) {   // diag (VTD_GEMM_VARIANT=3): no stores
+    epilogue_fast<EPI, true>(acc, reinterpret_cast<float*>(smem) + wave * 32 * 68, lane,
+                             m0 + wm * 128, n0 + wn * 64, e);
+    return;
+  }
+  if constexpr (kDiagSkipEpilogue) {         // timing diagnostic only (VTD_GEMM_VARIANT=2)
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (s != s) static_cast<float*>(e.out)[tid] = s;
+    return;
+  }
+  float* ep = reinterpret_cast<float*>(smem) + wave * 32 * 68;
+  const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
+  if constexpr (EPI != EPI_GENERIC) {
+    if (m0 + BBM <= M && n0 + BBN <= N) {
+      epilogue_fast<EPI>(acc, ep, lane, m_base, n_base, e);
+      return;
+    }
+  }
+  epilogue_generic(acc, ep, lane, M, N, m_base, n_base, e);
+}
+
 }  // namespace
 
 int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
@@ -363,13 +649,61 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
   if (dtype == VTD_BF16 && tiles_m * tiles_n >= 128) {
     static bool attr = false;
     if (!attr) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_bf16_256_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
+      const void* fns[] = {
+          reinterpret_cast<const void*>(&gemm_tn_bf16_256_kernel),
+          reinterpret_cast<const void*>(&gemm_tn_bf16_pingpong_kernel<EPI_GENERIC, true>),
+          reinterpret_cast<const void*>(&gemm_tn_bf16_pingpong_kernel<EPI_GENERIC, false>),
+          reinterpret_cast<const void*>(&gemm_tn_bf16_pingpong_kernel<4, true>),
+#define VTD_PP_FN(C) reinterpret_cast<const void*>(&gemm_tn_bf16_pingpong_kernel<C, false>),
+          VTD_PP_FN(0) VTD_PP_FN(1) VTD_PP_FN(2) VTD_PP_FN(4) VTD_PP_FN(5) VTD_PP_FN(6)
+          VTD_PP_FN(8) VTD_PP_FN(9) VTD_PP_FN(10) VTD_PP_FN(12) VTD_PP_FN(13) VTD_PP_FN(14)
+#undef VTD_PP_FN
+      };
+      for (const void* f : fns)
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
       attr = true;
     }
-    hipLaunchKernelGGL(gemm_tn_bf16_256_kernel, dim3(tiles_m * tiles_n), dim3(BNT),
-                       2 * BSTAGE, stream, M, N, K, static_cast<const bf16_t*>(A), lda,
-                       static_cast<const bf16_t*>(Bt), ldb, tiles_m, tiles_n, e);
+    static const int variant = [] {
+      const char* v = getenv("VTD_GEMM_VARIANT");
+      return v ? atoi(v) : 1;
+    }();
+    const dim3 g(tiles_m * tiles_n), b(BNT);
+    const bf16_t* a16 = static_cast<const bf16_t*>(A);
+    const bf16_t* b16 = static_cast<const bf16_t*>(Bt);
+    if (variant == 0) {
+      hipLaunchKernelGGL(gemm_tn_bf16_256_kernel, g, b, 2 * BSTAGE, stream, M, N, K, a16,
+                         lda, b16, ldb, tiles_m, tiles_n, e);
+    } else if (variant == 2) {
+      hipLaunchKernelGGL((gemm_tn_bf16_pingpong_kernel<EPI_GENERIC, true>), g, b, 2 * BSTAGE,
+                         stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);
+    } else if (variant == 3) {
+      hipLaunchKernelGGL((gemm_tn_bf16_pingpong_kernel<4, true>), g, b, 2 * BSTAGE,
+                         stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);
+    } else {
+      const bool fast = e.bias && !e.rowadd && e.scatter_tokens <= 0 && !e.out2 &&
+                        e.ldo % 8 == 0 && (!e.resid || e.ldr % 8 == 0) &&
+                        reinterpret_cast<uintptr_t>(e.out) % 16 == 0 &&
+                        reinterpret_cast<uintptr_t>(e.bias) % 16 == 0 &&
+                        (!e.resid || reinterpret_cast<uintptr_t>(e.resid) % 16 == 0);
+      const int code = fast ? epi_code(e.act, e.out_dtype == VTD_BF16, e.resid != nullptr)
+                            : EPI_GENERIC;
+      switch (code) {
+#define VTD_PP_CASE(C)                                                                    \
+  case C:                                                                                 \
+    hipLaunchKernelGGL((gemm_tn_bf16_pingpong_kernel<C, false>), g, b, 2 * BSTAGE, stream, \
+                       M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);                 \
+    break;
+        VTD_PP_CASE(0) VTD_PP_CASE(1) VTD_PP_CASE(2)
+        VTD_PP_CASE(4) VTD_PP_CASE(5) VTD_PP_CASE(6)
+        VTD_PP_CASE(8) VTD_PP_CASE(9) VTD_PP_CASE(10)
+        VTD_PP_CASE(12) VTD_PP_CASE(13) VTD_PP_CASE(14)
+#undef VTD_PP_CASE
+        default:
+          hipLaunchKernelGGL((gemm_tn_bf16_pingpong_kernel<EPI_GENERIC, false>), g, b,
+                             2 * BSTAGE, stream, M, N, K, a16, lda, b16, ldb, tiles_m,
+                             tiles_n, e);
+      }
+    }
   } else if (dtype == VTD_BF16)
     hipLaunchKernelGGL(gemm_tn_kernel<bf16_t>, grid, dim3(NT), lds, stream, M, N, K,
                        static_cast<const bf16_t*>(A), lda,
