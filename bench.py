@@ -114,12 +114,13 @@ def main():
     B = args.batch
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     images = letterbox_images(B, shape, gen, dev)
-    gathered = torch.empty((world * B, 17, 6), dtype=torch.float32, device=dev)
+
+    from vision_transformer_detector_amd.distributed import all_gather_detections
 
     def step():
         logits, dets = model.detect(images)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, dets)
+        if world > 1:                        # the path's one exchange: RCCL all-gather
+            all_gather_detections(dets, world * B)
         return logits
 
     for _ in range(args.warmup):
