@@ -164,10 +164,11 @@ __global__ __launch_bounds__(512) void attention_kernel(
       if constexpr (sizeof(T) == 2) {
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
-          bf16x8 pb;
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            pb[j] = static_cast<short>(f32_to_bf16(s[kb][8 * st + j]));
+          const bf16x8 pb = __builtin_bit_cast(
+              bf16x8, i32x4{(int)pack_bf16x2(s[kb][8 * st + 0], s[kb][8 * st + 1]),
+                            (int)pack_bf16x2(s[kb][8 * st + 2], s[kb][8 * st + 3]),
+                            (int)pack_bf16x2(s[kb][8 * st + 4], s[kb][8 * st + 5]),
+                            (int)pack_bf16x2(s[kb][8 * st + 6], s[kb][8 * st + 7])});
           const int key_lo = kb * 32 + 16 * st + 4 * half;   // j = 0..3
 #pragma unroll
           for (int db = 0; db < C::DB; ++db) {
@@ -208,10 +209,9 @@ __global__ __launch_bounds__(512) void attention_kernel(
     for (int g = 0; g < 4; ++g) {
       const int d = db * 32 + 8 * g + 4 * half;
       if constexpr (sizeof(T) == 2) {
-        bf16x4 v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = static_cast<short>(f32_to_bf16(o[db][4 * g + r] * inv));
-        *reinterpret_cast<bf16x4*>(op + d) = v;
+        const uint2 v = {pack_bf16x2(o[db][4 * g + 0] * inv, o[db][4 * g + 1] * inv),
+                         pack_bf16x2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv)};
+        *reinterpret_cast<uint2*>(op + d) = v;
       } else {
         f32x4 v;
 #pragma unroll

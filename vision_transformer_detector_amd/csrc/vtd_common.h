@@ -53,12 +53,16 @@ typedef __attribute__((ext_vector_type(4))) int i32x4;   // 16-B raw chunk
 __device__ __forceinline__ float bf16_to_f32(bf16_t v) {
   return __uint_as_float(static_cast<uint32_t>(v) << 16);
 }
-// round-to-nearest-even; NaN stays NaN
+// round-to-nearest-even via the hardware v_cvt_pk_bf16_f32 (a plain cast at -O3);
+// NaN stays NaN.
+typedef __bf16 bf16x2_hw __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ bf16_t f32_to_bf16(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return static_cast<bf16_t>((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return static_cast<bf16_t>(u >> 16);
+  return __builtin_bit_cast(bf16_t, static_cast<__bf16>(f));
+}
+// two floats -> packed bf16 pair (lo = a), one v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2_hw));
 }
 
 template <typename T> struct DT;
@@ -76,18 +80,21 @@ template <> struct DT<bf16_t> {
 // ----------------------------------------------------------------- activations
 // tfa.activations.mish = x * tanh(softplus(x)) (vtd.py:128-129).
 // tanh(log(1+e^x)) = n / (n + 2) with n = e^x (e^x + 2): no cancellation for x << 0.
+// v_exp_f32 / v_rcp_f32 (~1 ulp): 8 VALU, 2 of them transcendental.
 __device__ __forceinline__ float act_mish(float x) {
-  if (x > 20.f) return x;                      // tanh(softplus(x)) == 1 in fp32
-  float e = __expf(x);
-  float n = e * (e + 2.f);
-  return x * __fdividef(n, n + 2.f);
+  const float e = __builtin_amdgcn_exp2f(x * 1.4426950408889634f);
+  const float n = e * (e + 2.f);
+  const float y = x * n * __builtin_amdgcn_rcpf(n + 2.f);
+  return x > 20.f ? x : y;                     // tanh(softplus(x)) == 1 in fp32
 }
 // tfa GELU approximate=True: 0.5 x (1 + tanh(u)), u = sqrt(2/pi) (x + 0.044715 x^3)
-// == x * sigmoid(2u).
+// == x * sigmoid(2u) = x / (1 + 2^(x (c0 + c1 x^2))), c0 = -2 sqrt(2/pi) log2(e),
+// c1 = 0.044715 c0: 7 VALU, 2 transcendental; saturates correctly (inf -> 0, 0 -> x).
 __device__ __forceinline__ float act_gelu(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float u = k0 * (x + k1 * x * x * x);
-  return __fdividef(x, 1.f + __expf(-2.f * u));
+  constexpr float c0 = -2.f * 0.7978845608028654f * 1.4426950408889634f;
+  constexpr float c1 = c0 * 0.044715f;
+  const float e = __builtin_amdgcn_exp2f(x * __builtin_fmaf(c1, x * x, c0));
+  return x * __builtin_amdgcn_rcpf(1.f + e);
 }
 __device__ __forceinline__ float apply_act(int act, float x) {
   if (act == VTD_ACT_GELU_TANH) return act_gelu(x);

@@ -13,6 +13,8 @@
 // ds_read_b128 lane group spread over the banks.
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "vtd_common.h"
 
 namespace vtd {
@@ -377,38 +379,41 @@ __device__ __forceinline__ float act_ct(float x) {
 // Writes the wave's 128 x 64 accumulator tile: 4 passes of 32 rows staged through the
 // wave's private LDS region; each lane then owns 8 consecutive columns of a row, so
 // residual reads and output writes are 16-B per lane (one 128-B line per 8 lanes).
-template <int EPI, bool kDiagNoStore = false>
+template <int EPI, bool kDiagNoStore = false, int PR = 32>
 __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* ep, int lane,
                                               int m_base, int n_base, const EpiArgs& e) {
   constexpr int ACT = EPI & 3;
   constexpr bool OUT_BF16 = (EPI & 4) != 0;
   constexpr bool RESID = (EPI & 8) != 0;
   constexpr int ES = 68;
+  constexpr int NB = PR / 16;            // accumulator row blocks per pass
+  constexpr int NIT = PR / 8;            // row-vector iterations per pass
   const int fr = lane & 15, fg = lane >> 4;
   const int c8 = (lane & 7) * 8, rsub = lane >> 3;
   const f32x4 b0 = *reinterpret_cast<const f32x4*>(e.bias + n_base + c8);
   const f32x4 b1 = *reinterpret_cast<const f32x4*>(e.bias + n_base + c8 + 4);
+  if (e.scatter_tokens == -2) m_base &= 255;   // timing diagnostic (VTD_GEMM_VARIANT=5)
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
+  for (int p = 0; p < 128 / PR; ++p) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NB; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r2 = 0; r2 < 4; ++r2)
-          ep[(i * 16 + fg * 4 + r2) * ES + j * 16 + fr] = acc[p * 2 + i][j][r2];
-    f32x4 rv[4][2];
+          ep[(i * 16 + fg * 4 + r2) * ES + j * 16 + fr] = acc[p * NB + i][j][r2];
+    f32x4 rv[NIT][2];
     if constexpr (RESID) {
 #pragma unroll
-      for (int it = 0; it < 4; ++it) {
-        const int64_t m = m_base + p * 32 + it * 8 + rsub;
+      for (int it = 0; it < NIT; ++it) {
+        const int64_t m = m_base + p * PR + it * 8 + rsub;
         const float* rp = e.resid + m * e.ldr + n_base + c8;
         rv[it][0] = *reinterpret_cast<const f32x4*>(rp);
         rv[it][1] = *reinterpret_cast<const f32x4*>(rp + 4);
       }
     }
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
+    for (int it = 0; it < NIT; ++it) {
       const int row = it * 8 + rsub;
       f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + row * ES + c8) + b0;
       f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + row * ES + c8 + 4) + b1;
@@ -421,17 +426,13 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
         v0 += rv[it][0];
         v1 += rv[it][1];
       }
-      const int64_t idx = (int64_t)(m_base + p * 32 + row) * e.ldo + n_base + c8;
+      const int64_t idx = (int64_t)(m_base + p * PR + row) * e.ldo + n_base + c8;
       if constexpr (kDiagNoStore) {
         if (v0[0] != v0[0] && v1[3] != v1[3]) static_cast<float*>(e.out)[idx] = v0[1];
       } else if constexpr (OUT_BF16) {
-        bf16x8 o;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          o[j] = static_cast<short>(f32_to_bf16(v0[j]));
-          o[j + 4] = static_cast<short>(f32_to_bf16(v1[j]));
-        }
-        *reinterpret_cast<bf16x8*>(static_cast<bf16_t*>(e.out) + idx) = o;
+        const i32x4 o = {(int)pack_bf16x2(v0[0], v0[1]), (int)pack_bf16x2(v0[2], v0[3]),
+                         (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
+        *reinterpret_cast<i32x4*>(static_cast<bf16_t*>(e.out) + idx) = o;
       } else {
         float* op = static_cast<float*>(e.out) + idx;
         *reinterpret_cast<f32x4*>(op) = v0;
@@ -440,36 +441,44 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
     }
   }
 }
+// global stores the fast epilogue issues per wave (used for counted vmcnt waits)
+template <int EPI, int PR = 32>
+constexpr int epilogue_fast_stores() {
+  return (128 / PR) * (PR / 8) * ((EPI & 4) ? 1 : 2);
+}
 
 // Runtime-flag epilogue for partial tiles and rare modes (rowadd, scatter, out2): the
 // accumulators are staged into LDS inline (static register indices), and only the
 // LDS -> global loop is kept rolled (keeps the kernel small).
+template <int PR = 32>
 __device__ __forceinline__ void epilogue_generic_pass(const float* ep, int lane, int M, int N,
-                                                   int m_base, int n_base, const EpiArgs& e) {
+                                                      int m_base, int n_base, const EpiArgs& e) {
   constexpr int ES = 68;
 #pragma unroll 1
-  for (int it = 0; it < 8; ++it) {
+  for (int it = 0; it < PR / 4; ++it) {
     const int row = it * 4 + (lane >> 4), col = (lane & 15) * 4;
     const f32x4 v = *reinterpret_cast<const f32x4*>(ep + row * ES + col);
     epi_store4(e, M, N, m_base + row, n_base + col, v);
   }
 }
 
+template <int PR = 32>
 __device__ __forceinline__ void epilogue_generic(const f32x4 (&acc)[8][4], float* ep, int lane,
                                                  int M, int N, int m_base, int n_base,
                                                  const EpiArgs& e) {
   constexpr int ES = 68;
+  constexpr int NB = PR / 16;
   const int fr = lane & 15, fg = lane >> 4;
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
+  for (int p = 0; p < 128 / PR; ++p) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NB; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r2 = 0; r2 < 4; ++r2)
-          ep[(i * 16 + fg * 4 + r2) * ES + j * 16 + fr] = acc[p * 2 + i][j][r2];
-    epilogue_generic_pass(ep, lane, M, N, m_base + p * 32, n_base, e);
+          ep[(i * 16 + fg * 4 + r2) * ES + j * 16 + fr] = acc[p * NB + i][j][r2];
+    epilogue_generic_pass<PR>(ep, lane, M, N, m_base + p * PR, n_base, e);
   }
 }
 
@@ -511,6 +520,56 @@ __device__ __forceinline__ void pp_load_b(bf16x8 (&b)[2][2], const char* lb, int
 #pragma unroll
     for (int s = 0; s < 2; ++s)
       b[j][s] = *reinterpret_cast<const bf16x8*>(lb + swz(row0 + j * 16 + fr, 4 * s + fg));
+}
+
+// The ping-pong K loop.  Precondition: K-tile 0 is in stage 0 and visible to all waves
+// (its DMA drained and a workgroup barrier passed).  Postcondition: every wave has
+// finished every section (re-aligned), all DMA of this loop has landed.
+__device__ __forceinline__ void pp_mainloop(f32x4 (&acc)[8][4], char* smem,
+                                            const char* const (&srcA)[4],
+                                            const char* const (&srcB)[4], int lds_piece,
+                                            int nk, int wm, int arow, int brow, int fr,
+                                            int fg) {
+  if (wm == 1) pp_barrier();                 // stagger G1 by one barrier
+  bf16x8 a[4][2], b0[2][2], b1[2][2];
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* la = smem + (kt & 1) * BSTAGE;
+    const char* lb = la + BBM * KB;
+    char* nxt = smem + ((kt + 1) & 1) * BSTAGE;
+    const bool pf = kt + 1 < nk;
+    const int64_t ko = (int64_t)(kt + 1) * KB;
+    // ---- P0
+    pp_load_a(a, la, arow, fr, fg);
+    pp_load_b(b0, lb, brow, fr, fg);
+    if (pf) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) glds16(srcA[j] + ko, nxt + lds_piece + j * 8 * KB);
+    }
+    pp_barrier();
+    pp_mfma<0, 0>(acc, a, b0);
+    pp_barrier();
+    // ---- P1
+    pp_load_b(b1, lb, brow + 32, fr, fg);
+    if (pf) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        glds16(srcB[j] + ko, nxt + BBM * KB + lds_piece + j * 8 * KB);
+    }
+    pp_barrier();
+    pp_mfma<0, 2>(acc, a, b1);
+    pp_barrier();
+    // ---- P2
+    pp_load_a(a, la, arow + 64, fr, fg);
+    pp_barrier();
+    pp_mfma<4, 2>(acc, a, b1);
+    pp_barrier();
+    // ---- P3
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pp_barrier();
+    pp_mfma<4, 0>(acc, a, b0);
+    pp_barrier();
+  }
+  if (wm == 0) pp_barrier();                 // re-align: every wave past its last section
 }
 
 template <int EPI, bool kDiagSkipEpilogue>
@@ -556,47 +615,7 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pingpong_kernel(
   issue_tile(smem, srcA, srcB, lds_piece, 0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   pp_barrier();
-  if (wm == 1) pp_barrier();                 // stagger G1 by one barrier
-
-  bf16x8 a[4][2], b0[2][2], b1[2][2];
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* la = smem + (kt & 1) * BSTAGE;
-    const char* lb = la + BBM * KB;
-    char* nxt = smem + ((kt + 1) & 1) * BSTAGE;
-    const bool pf = kt + 1 < nk;
-    const int64_t ko = (int64_t)(kt + 1) * KB;
-    // ---- P0
-    pp_load_a(a, la, arow, fr, fg);
-    pp_load_b(b0, lb, brow, fr, fg);
-    if (pf) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) glds16(srcA[j] + ko, nxt + lds_piece + j * 8 * KB);
-    }
-    pp_barrier();
-    pp_mfma<0, 0>(acc, a, b0);
-    pp_barrier();
-    // ---- P1
-    pp_load_b(b1, lb, brow + 32, fr, fg);
-    if (pf) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        glds16(srcB[j] + ko, nxt + BBM * KB + lds_piece + j * 8 * KB);
-    }
-    pp_barrier();
-    pp_mfma<0, 2>(acc, a, b1);
-    pp_barrier();
-    // ---- P2
-    pp_load_a(a, la, arow + 64, fr, fg);
-    pp_barrier();
-    pp_mfma<4, 2>(acc, a, b1);
-    pp_barrier();
-    // ---- P3
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    pp_barrier();
-    pp_mfma<4, 0>(acc, a, b0);
-    pp_barrier();
-  }
-  if (wm == 0) pp_barrier();                 // re-align: every wave past its last section
+  pp_mainloop(acc, smem, srcA, srcB, lds_piece, nk, wm, arow, brow, fr, fg);
 
   if constexpr (kDiagSkipEpilogue && EPI >= 0) {   // diag (VTD_GEMM_VARIANT=3): no stores
     epilogue_fast<EPI, true>(acc, reinterpret_cast<float*>(smem) + wave * 32 * 68, lane,
@@ -621,6 +640,100 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pingpong_kernel(
     }
   }
   epilogue_generic(acc, ep, lane, M, N, m_base, n_base, e);
+}
+
+
+// ============================================================================
+// Persistent variant of the ping-pong kernel: gridDim.x blocks (one per CU) walk the
+// tiles t = blockIdx.x, +gridDim.x, ...  After a tile's K loop the block issues the DMA
+// of the NEXT tile's K-tile 0 into stage 0, then runs this tile's epilogue staged in
+// stage 1 (16-row passes, 34.8 KiB) and continues without draining its stores: the
+// next tile's first wait is vmcnt(#epilogue stores) (those are younger than the DMA), so
+// the stores drain while the next tile's first K-tile is computed.
+// ============================================================================
+template <int EPI>
+__global__ __launch_bounds__(BNT) void gemm_tn_bf16_persistent_kernel(
+    int M, int N, int K, const bf16_t* __restrict__ A, int lda,
+    const bf16_t* __restrict__ Bt, int ldb, int tiles_m, int tiles_n, EpiArgs e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int nk = K / 64;
+  const int arow = wm * 128, brow = wn * 64;
+  const int nwg = tiles_m * tiles_n;
+  const int q = nwg >> 3, r = nwg & 7;
+  const int prow = lane >> 3;
+  const int pchunk = (lane & 7) ^ prow;
+  const int lds_piece = wave * 32 * KB;
+  float* ep = reinterpret_cast<float*>(smem + BSTAGE) + wave * 16 * 68;
+  constexpr int PR = 16;
+
+  auto tile_origin = [&](int t, int& m0, int& n0) {
+    const int x = t & 7;
+    const int tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (t >> 3);
+    const int tm = tile / tiles_n;
+    m0 = tm * BBM;
+    n0 = (tile - tm * tiles_n) * BBN;
+  };
+  auto sources = [&](int m0, int n0, const char* (&sa)[4], const char* (&sb)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = wave * 32 + j * 8 + prow;
+      sa[j] = reinterpret_cast<const char*>(A + (int64_t)min(m0 + row, M - 1) * lda) + pchunk * 16;
+      sb[j] = reinterpret_cast<const char*>(Bt + (int64_t)min(n0 + row, N - 1) * ldb) + pchunk * 16;
+    }
+  };
+
+  int t = blockIdx.x;
+  if (t >= nwg) return;
+  int m0, n0;
+  tile_origin(t, m0, n0);
+  const char* srcA[4];
+  const char* srcB[4];
+  sources(m0, n0, srcA, srcB);
+  issue_tile(smem, srcA, srcB, lds_piece, 0, 0);
+  int pending_stores = 0;                    // epilogue stores younger than the DMA
+  for (;;) {
+    if (pending_stores == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(epilogue_fast_stores<(EPI < 0 ? 0 : EPI), 16>()) : "memory");
+    pp_barrier();
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    pp_mainloop(acc, smem, srcA, srcB, lds_piece, nk, wm, arow, brow, fr, fg);
+
+    const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
+    const bool full = m0 + BBM <= M && n0 + BBN <= N;
+    const int tn = t + gridDim.x;
+    const int cm0 = m0, cn0 = n0;
+    if (tn < nwg) {                          // next tile's K-tile 0 -> stage 0 (free)
+      tile_origin(tn, m0, n0);
+      sources(m0, n0, srcA, srcB);
+      issue_tile(smem, srcA, srcB, lds_piece, 0, 0);
+    }
+    (void)cm0; (void)cn0;
+    if constexpr (EPI != EPI_GENERIC) {
+      if (full) {
+        epilogue_fast<EPI, false, PR>(acc, ep, lane, m_base, n_base, e);
+        pending_stores = 1;
+      } else {
+        epilogue_generic<PR>(acc, ep, lane, M, N, m_base, n_base, e);
+        pending_stores = 0;
+      }
+    } else {
+      epilogue_generic<PR>(acc, ep, lane, M, N, m_base, n_base, e);
+      pending_stores = 0;
+    }
+    if (tn >= nwg) break;
+    t = tn;
+    // every wave's staging reads of stage 1 are done before the next K loop DMAs into it
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
 }
 
 }  // namespace
@@ -654,7 +767,9 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
           reinterpret_cast<const void*>(&gemm_tn_bf16_pingpong_kernel<EPI_GENERIC, true>),
           reinterpret_cast<const void*>(&gemm_tn_bf16_pingpong_kernel<EPI_GENERIC, false>),
           reinterpret_cast<const void*>(&gemm_tn_bf16_pingpong_kernel<4, true>),
-#define VTD_PP_FN(C) reinterpret_cast<const void*>(&gemm_tn_bf16_pingpong_kernel<C, false>),
+          reinterpret_cast<const void*>(&gemm_tn_bf16_persistent_kernel<EPI_GENERIC>),
+#define VTD_PP_FN(C) reinterpret_cast<const void*>(&gemm_tn_bf16_pingpong_kernel<C, false>), \
+                     reinterpret_cast<const void*>(&gemm_tn_bf16_persistent_kernel<C>),
           VTD_PP_FN(0) VTD_PP_FN(1) VTD_PP_FN(2) VTD_PP_FN(4) VTD_PP_FN(5) VTD_PP_FN(6)
           VTD_PP_FN(8) VTD_PP_FN(9) VTD_PP_FN(10) VTD_PP_FN(12) VTD_PP_FN(13) VTD_PP_FN(14)
 #undef VTD_PP_FN
@@ -680,18 +795,31 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
       hipLaunchKernelGGL((gemm_tn_bf16_pingpong_kernel<4, true>), g, b, 2 * BSTAGE,
                          stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);
     } else {
-      const bool fast = e.bias && !e.rowadd && e.scatter_tokens <= 0 && !e.out2 &&
+      const bool fast = e.bias && !e.rowadd && (e.scatter_tokens <= 0 || variant == 5) && !e.out2 &&
                         e.ldo % 8 == 0 && (!e.resid || e.ldr % 8 == 0) &&
                         reinterpret_cast<uintptr_t>(e.out) % 16 == 0 &&
                         reinterpret_cast<uintptr_t>(e.bias) % 16 == 0 &&
                         (!e.resid || reinterpret_cast<uintptr_t>(e.resid) % 16 == 0);
       const int code = fast ? epi_code(e.act, e.out_dtype == VTD_BF16, e.resid != nullptr)
                             : EPI_GENERIC;
+      static const int num_cu = [] {
+        int dev = 0, n = 256;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        return n;
+      }();
+      const bool persistent = variant == 4;
+      if (variant == 5) e.scatter_tokens = -2;      // diag: all tiles store to rows 0..255
+      const dim3 gp(std::min(tiles_m * tiles_n, num_cu));
       switch (code) {
-#define VTD_PP_CASE(C)                                                                    \
-  case C:                                                                                 \
-    hipLaunchKernelGGL((gemm_tn_bf16_pingpong_kernel<C, false>), g, b, 2 * BSTAGE, stream, \
-                       M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);                 \
+#define VTD_PP_CASE(C)                                                                      \
+  case C:                                                                                   \
+    if (persistent)                                                                         \
+      hipLaunchKernelGGL((gemm_tn_bf16_persistent_kernel<C>), gp, b, 2 * BSTAGE, stream, M, \
+                         N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);                    \
+    else                                                                                    \
+      hipLaunchKernelGGL((gemm_tn_bf16_pingpong_kernel<C, false>), g, b, 2 * BSTAGE, stream, \
+                         M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);                 \
     break;
         VTD_PP_CASE(0) VTD_PP_CASE(1) VTD_PP_CASE(2)
         VTD_PP_CASE(4) VTD_PP_CASE(5) VTD_PP_CASE(6)
@@ -699,9 +827,14 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
         VTD_PP_CASE(12) VTD_PP_CASE(13) VTD_PP_CASE(14)
 #undef VTD_PP_CASE
         default:
-          hipLaunchKernelGGL((gemm_tn_bf16_pingpong_kernel<EPI_GENERIC, false>), g, b,
-                             2 * BSTAGE, stream, M, N, K, a16, lda, b16, ldb, tiles_m,
-                             tiles_n, e);
+          if (persistent)
+            hipLaunchKernelGGL((gemm_tn_bf16_persistent_kernel<EPI_GENERIC>), gp, b,
+                               2 * BSTAGE, stream, M, N, K, a16, lda, b16, ldb, tiles_m,
+                               tiles_n, e);
+          else
+            hipLaunchKernelGGL((gemm_tn_bf16_pingpong_kernel<EPI_GENERIC, false>), g, b,
+                               2 * BSTAGE, stream, M, N, K, a16, lda, b16, ldb, tiles_m,
+                               tiles_n, e);
       }
     }
   } else if (dtype == VTD_BF16)
