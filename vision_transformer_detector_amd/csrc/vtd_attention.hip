@@ -15,6 +15,8 @@
 //   f32 : v_mfma_f32_32x32x2_f32  (1 element per lane per operand)
 // Generic lane map used by both (E = elements per lane): lane half h = l >> 5 supplies
 // k = 2E*step + h*E + j; accumulator register rho holds row (rho&3) + 8(rho>>2) + 4h.
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "vtd_common.h"
@@ -221,6 +223,200 @@ __global__ __launch_bounds__(512) void attention_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------
+// bf16 kernel, v2: K and V are staged row-major with 16-B stores (global -> registers
+// during the previous chunk's compute -> LDS after it; two LDS buffers, one barrier per
+// 64-key chunk).  The A operand of O^T += V^T P^T needs, per lane (d = l & 31 of the
+// 32-wide d block, half h = l >> 5), the 8 keys 16s + 8(j>>2) + 4h + (j&3) of column d:
+// two ds_read_b64_tr_b16, each delivering one column of a 4-key x 16-d block
+// (lane 4q+p of a 16-lane group addresses key q, d 4p..4p+3 of the block).
+// V row stride DKP*2 + 64 B shifts consecutive keys by 16 mod 64 banks, so the 4 rows
+// x 64 B of a 32-lane tr-read half cover all 64 banks once (conflict-free for DKP 64/128).
+template <int DKP>
+struct AttnBf16Cfg {
+  static constexpr int KC = 64;                       // keys per chunk
+  static constexpr int KS = DKP * 2 + 16;             // K row stride (bytes)
+  static constexpr int VS = DKP * 2 + 64;             // V row stride (bytes)
+  static constexpr int BUF = KC * KS + KC * VS;
+  static constexpr int CPR = DKP * 2 / 16;            // 16-B chunks per row
+  static constexpr int NCH = KC * CPR * 2;            // chunks per K+V tile
+  static constexpr int KSTEPS = DKP / 16;
+  static constexpr int DB = DKP / 32;
+};
+
+template <int DKP, int NWG>
+__global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void attention_bf16_kernel(
+    const bf16_t* __restrict__ qkv, int N, int heads, int ldqkv, float scale_log2,
+    bf16_t* __restrict__ out, int ldo) {
+  using C = AttnBf16Cfg<DKP>;
+  typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  constexpr int nthreads = 64 * NWG;
+  const int lane = tid & 63, wave = tid >> 6, half = lane >> 5, col = lane & 31;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int inner = heads * DKP;
+  const int64_t row0 = (int64_t)b * N;
+  const int q0 = (blockIdx.x * NWG + wave) * 32;
+  const bool active = q0 < N;
+
+  bf16x8 qf[C::KSTEPS];
+  {
+    const int q = min(q0 + col, N - 1);
+    const bf16_t* qp = qkv + (row0 + q) * ldqkv + h * DKP;
+#pragma unroll
+    for (int st = 0; st < C::KSTEPS; ++st)
+      qf[st] = *reinterpret_cast<const bf16x8*>(qp + st * 16 + half * 8);
+  }
+  f32x16 o[C::DB];
+#pragma unroll
+  for (int i = 0; i < C::DB; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+
+  constexpr int NPASS = (C::NCH + nthreads - 1) / nthreads;
+  i32x4 stg[NPASS];
+  auto gload = [&](int kv0) {
+#pragma unroll
+    for (int i = 0; i < NPASS; ++i) {
+      const int c = tid + i * nthreads;
+      if (c < C::NCH) {
+        const int isv = c >= C::KC * C::CPR;
+        const int cc = c - isv * C::KC * C::CPR;
+        const int kr = cc / C::CPR, ch = cc - kr * C::CPR;
+        const int key = min(kv0 + kr, N - 1);
+        stg[i] = *reinterpret_cast<const i32x4*>(qkv + (row0 + key) * ldqkv +
+                                                 (1 + isv) * inner + h * DKP + ch * 8);
+      }
+    }
+  };
+  auto swrite = [&](int buf) {
+    char* base = smem + buf * C::BUF;
+#pragma unroll
+    for (int i = 0; i < NPASS; ++i) {
+      const int c = tid + i * nthreads;
+      if (c < C::NCH) {
+        const int isv = c >= C::KC * C::CPR;
+        const int cc = c - isv * C::KC * C::CPR;
+        const int kr = cc / C::CPR, ch = cc - kr * C::CPR;
+        char* dst = isv ? base + C::KC * C::KS + kr * C::VS + ch * 16 : base + kr * C::KS + ch * 16;
+        *reinterpret_cast<i32x4*>(dst) = stg[i];
+      }
+    }
+  };
+
+  const int nchunks = (N + C::KC - 1) / C::KC;
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  // per-lane tr-read address pieces: key offset within a 4-key block, d offset
+  const int tr_key = 4 * half + ((lane & 15) >> 2);
+  const int tr_d = ((lane >> 4) & 1) * 16 + (lane & 3) * 4;
+  for (int c = 0; c < nchunks; ++c) {
+    const int kv0 = c * C::KC;
+    if (c + 1 < nchunks) gload(kv0 + C::KC);
+    if (active) {
+      const char* kl = smem + (c & 1) * C::BUF;
+      const char* vl = kl + C::KC * C::KS;
+      f32x16 s[2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+        const char* krow = kl + (kb * 32 + col) * C::KS;
+#pragma unroll
+        for (int st = 0; st < C::KSTEPS; ++st)
+          s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              *reinterpret_cast<const bf16x8*>(krow + (st * 16 + half * 8) * 2), qf[st], s[kb],
+              0, 0, 0);
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kv0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+          const float v = key < N ? s[kb][r] * scale_log2 : -INFINITY;
+          s[kb][r] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+      m_run = m_new;
+      float psum = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = __builtin_amdgcn_exp2f(s[kb][r] - m_new);
+          s[kb][r] = p;
+          psum += p;
+        }
+      l_run = l_run * alpha + psum;
+#pragma unroll
+      for (int i = 0; i < C::DB; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const bf16x8 pb = __builtin_bit_cast(
+              bf16x8, i32x4{(int)pack_bf16x2(s[kb][8 * st + 0], s[kb][8 * st + 1]),
+                            (int)pack_bf16x2(s[kb][8 * st + 2], s[kb][8 * st + 3]),
+                            (int)pack_bf16x2(s[kb][8 * st + 4], s[kb][8 * st + 5]),
+                            (int)pack_bf16x2(s[kb][8 * st + 6], s[kb][8 * st + 7])});
+          const int key0 = kb * 32 + 16 * st + tr_key;
+#pragma unroll
+          for (int db = 0; db < C::DB; ++db) {
+            const char* va = vl + key0 * C::VS + (db * 32 + tr_d) * 2;
+            const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)va);
+            const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(va + 8 * C::VS));
+            const bf16x8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb, o[db], 0, 0, 0);
+          }
+        }
+    }
+    if (c + 1 < nchunks) swrite((c + 1) & 1);
+    __syncthreads();
+  }
+  if (!active) return;
+  const float inv = 1.f / (l_run + __shfl_xor(l_run, 32));
+  const int q = q0 + col;
+  if (q >= N) return;
+  bf16_t* op = out + (row0 + q) * ldo + h * DKP;
+#pragma unroll
+  for (int db = 0; db < C::DB; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = db * 32 + 8 * g + 4 * half;
+      const uint2 v = {pack_bf16x2(o[db][4 * g + 0] * inv, o[db][4 * g + 1] * inv),
+                       pack_bf16x2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv)};
+      *reinterpret_cast<uint2*>(op + d) = v;
+    }
+}
+
+template <int DKP, int NWG>
+int launch_bf16_v2(const void* qkv, int B, int N, int heads, int ldqkv, float scale,
+                   void* out, int ldo, hipStream_t stream) {
+  using C = AttnBf16Cfg<DKP>;
+  const int nq = (N + 31) / 32;
+  dim3 grid((nq + NWG - 1) / NWG, heads, B);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_bf16_kernel<DKP, NWG>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 2 * C::BUF);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((attention_bf16_kernel<DKP, NWG>), grid, dim3(64 * NWG), 2 * C::BUF,
+                     stream, static_cast<const bf16_t*>(qkv), N, heads, ldqkv,
+                     scale * 1.4426950408889634f, static_cast<bf16_t*>(out), ldo);
+  VTD_LAUNCH_CHECK("attention_bf16");
+  return VTD_OK;
+}
+
 template <typename T, int DKP>
 int launch(const void* qkv, int B, int N, int heads, int ldqkv, float scale, void* out,
            int ldo, hipStream_t stream) {
@@ -257,9 +453,23 @@ int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqk
   ProfScope ps(stream, PROF_ATTN,
                flops > 0 ? flops : 4.0 * B * heads * (double)N * N * dkp);
   if (dtype == VTD_BF16) {
-    if (dkp == 32) return launch<bf16_t, 32>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
-    if (dkp == 64) return launch<bf16_t, 64>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
-    return launch<bf16_t, 128>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+    static const int v1 = [] {
+      const char* v = getenv("VTD_ATTN_VARIANT");
+      return v ? atoi(v) : 2;
+    }();
+    if (v1 == 1) {
+      if (dkp == 32) return launch<bf16_t, 32>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+      if (dkp == 64) return launch<bf16_t, 64>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+      return launch<bf16_t, 128>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+    }
+    if (v1 == 3 || (v1 == 2 && N > 128)) {   // 8-wave workgroups (one (b,h) per WG to N=256)
+      if (dkp == 32) return launch_bf16_v2<32, 8>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+      if (dkp == 64) return launch_bf16_v2<64, 8>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+      return launch_bf16_v2<128, 8>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+    }
+    if (dkp == 32) return launch_bf16_v2<32, 4>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+    if (dkp == 64) return launch_bf16_v2<64, 4>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+    return launch_bf16_v2<128, 4>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
   }
   if (dkp == 32) return launch<float, 32>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
   if (dkp == 64) return launch<float, 64>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
