@@ -61,6 +61,43 @@ def algorithmic_flops_per_image(kw, dims):
     return total, L * (qkv + attn + out + mlp)
 
 
+def traffic_per_launch():
+    """HBM bytes per GEMM launch from the rocprofv3 PMC passes committed under
+    profiles/ (tools/pmc_traffic.py: FETCH_SIZE x 2 + WRITE_SIZE, separate passes of
+    this same bench command), or None when no such measurement exists."""
+    p = os.path.join(ROOT, "profiles", "gemm_traffic_latest.json")
+    try:
+        return round(json.load(open(p))["traffic_bytes_per_launch"])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def gemm_alg_bytes(kw, dims, b):
+    """Algorithmic bytes of one forward's GEMMs (each operand read once, output written
+    once, residual read once), averaged per GEMM launch: the `traffic` yardstick."""
+    rows, d = b * dims.tokens, kw["embedding_dim"]
+    inner = kw["encoder_num_heads"] * kw["encoder_key_dim"]
+    g = [(rows, d, dims.patch_dim, 4, False)]
+    for _ in range(kw["encoder_repeat_times"]):
+        g.append((rows, 3 * inner, d, 2, False))
+        g.append((rows, d, inner, 4, True))
+        k = d
+        for j in range(kw["encoder_mlp_quantities"]):
+            n = dims.mlp_units[j]
+            last = j == kw["encoder_mlp_quantities"] - 1
+            g.append((rows, n, k, 4 if last else 2, last))
+            k = n
+    g.append((rows, 17, d, 2, False))
+    hr, k = b * 17, dims.tokens
+    for j in range(dims.n_head):
+        g.append((hr, dims.head_units[j], k, 2, False))
+        k = dims.head_units[j]
+    g.append((hr, 6, k, 4, False))
+    tot = sum(2 * m * kk + 2 * n * kk + ob * m * n + (4 * m * n if r else 0)
+              for m, n, kk, ob, r in g)
+    return tot / len(g)
+
+
 def cpu_baseline(model, kw, shape, seconds=12.0):
     """The oracle's fp32 torch-CPU restatement (oracle/vtd_torch_cpu.py) of the same
     graph on the host cores: the reference's TF-CPU path cannot run in this pipeline
@@ -189,11 +226,12 @@ def main():
                    "parallelism": f"dp{world}"},
         "mfma_util_attn_mlp": round(attn_mlp_fl * img_s / world / (peak * 1e12), 4),
         "model_tflops_per_gpu": round(total_fl * img_s / world / 1e12, 1),
-        "roofline": {"bound": "mfma", "kernel": "gemm_tn_kernel (all Dense layers)",
+        "roofline": {"bound": "mfma", "kernel": "gemm_tn_bf16_* (all Dense layers)",
                      "achieved": round(gemm_tf, 1) if gemm_tf else None, "peak": peak,
                      "unit": "TFLOP/s",
                      "frac": round(gemm_tf / peak, 4) if gemm_tf else None,
-                     "traffic": None,
+                     "traffic": traffic_per_launch(),
+                     "algorithmic_bytes_per_launch": round(gemm_alg_bytes(kw, model.dims, B)),
                      "avg_launch_us": round(g["avg_us"], 2),
                      "launches_per_step": g["launches"] // max(1, args.steps)},
         "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv)

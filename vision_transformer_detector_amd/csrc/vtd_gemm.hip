@@ -572,6 +572,149 @@ __device__ __forceinline__ void pp_mainloop(f32x4 (&acc)[8][4], char* smem,
   if (wm == 0) pp_barrier();                 // re-align: every wave past its last section
 }
 
+// ---------------------------------------------------------------------------------
+// Ping-pong K loop v2: each 64 KiB stage holds four 16 KiB DMA groups, one per operand
+// quadrant a phase reads:  X0 = A rows {0-63, 128-191} (A quad 0 of both wave groups),
+// X1 = A rows {64-127, 192-255}, Y0 = B rows {0-31, 64-95, 128-159, 192-223} (B quad 0
+// of every wn), Y1 = the other B rows.  Group row gr -> LDS offset gr*128 + swizzled chunk.
+// A group is re-filled as soon as its last reader has retired, two tiles ahead:
+//   tile t, P0: DMA X1(t+1)  | reads X0(t), Y0(t) | wait vmcnt(10) -> Y1(t) landed
+//           P1:              | reads Y1(t)        | wait vmcnt(8)  -> X1(t) landed
+//           P2: DMA X0(t+2)  | reads X1(t)        |
+//           P3: DMA Y0,Y1(t+2)|                   | wait vmcnt(10) -> X0,Y0(t+1) landed
+// (2 DMA instructions per group per wave; waits count the younger DMA in issue order;
+// any phase whose younger DMA may be missing near the end of K waits vmcnt(0).)
+// WAR (event numbers as for the v1 loop): X1(t+1) overwrites X1(t-1), last read in
+// tile t-1's P2 (retired by event 8t-1) and issued after event 8t; X0(t+2) overwrites
+// X0(t) read in P0 (retired by 8t+3), issued after 8t+4; Y0/Y1(t+2) overwrite Y0/Y1(t)
+// read in P0/P1 (retired by 8t+5), issued after 8t+6.
+__device__ __forceinline__ int grp_tile_row(int g, int gr) {
+  return g < 2 ? (gr & 64) * 2 + g * 64 + (gr & 63)          // X0 / X1 (A rows)
+               : (gr >> 5) * 64 + (g - 2) * 32 + (gr & 31);  // Y0 / Y1 (B rows)
+}
+
+struct PP2Src {   // per-lane DMA sources of this tile: [group][piece]
+  const char* p[4][2];
+};
+
+__device__ __forceinline__ void pp2_sources(PP2Src& src, const bf16_t* A, int lda, int M,
+                                            const bf16_t* Bt, int ldb, int N, int m0, int n0,
+                                            int wave, int lane) {
+  const int prow = lane >> 3, pchunk = (lane & 7) ^ prow;
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int tr = grp_tile_row(g, (wave * 2 + j) * 8 + prow);
+      src.p[g][j] = g < 2
+          ? reinterpret_cast<const char*>(A + (int64_t)min(m0 + tr, M - 1) * lda) + pchunk * 16
+          : reinterpret_cast<const char*>(Bt + (int64_t)min(n0 + tr, N - 1) * ldb) + pchunk * 16;
+    }
+}
+
+template <int G>
+__device__ __forceinline__ void pp2_issue(char* smem, const PP2Src& src, int wave, int kt,
+                                          int stage) {
+  char* dst = smem + stage * BSTAGE + G * 16384 + wave * 2 * 1024;
+  const int64_t ko = (int64_t)kt * KB;
+  glds16(src.p[G][0] + ko, dst);
+  glds16(src.p[G][1] + ko, dst + 1024);
+}
+
+__device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, const PP2Src& src,
+                                             int nk, int wave, int wm, int wn, int fr, int fg) {
+  // prologue: tile 0 complete, tile 1's X0/Y0/Y1 in flight
+  pp2_issue<0>(smem, src, wave, 0, 0);
+  pp2_issue<2>(smem, src, wave, 0, 0);
+  pp2_issue<3>(smem, src, wave, 0, 0);
+  pp2_issue<1>(smem, src, wave, 0, 0);
+  if (nk > 1) {
+    pp2_issue<0>(smem, src, wave, 1, 1);
+    pp2_issue<2>(smem, src, wave, 1, 1);
+    pp2_issue<3>(smem, src, wave, 1, 1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  pp_barrier();
+  if (wm == 1) pp_barrier();                 // stagger G1 by one barrier
+  const int ra = wm * 64, rb = wn * 32;      // group rows of this wave's quads
+  bf16x8 a[4][2], b0[2][2], b1[2][2];
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* st = smem + (kt & 1) * BSTAGE;
+    const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+    // ---- P0
+    pp_load_a(a, st + 0 * 16384, ra, fr, fg);
+    pp_load_b(b0, st + 2 * 16384, rb, fr, fg);
+    if (n1) pp2_issue<1>(smem, src, wave, kt + 1, (kt + 1) & 1);
+    if (n1) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pp_barrier();
+    pp_mfma<0, 0>(acc, a, b0);
+    pp_barrier();
+    // ---- P1
+    pp_load_b(b1, st + 3 * 16384, rb, fr, fg);
+    if (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pp_barrier();
+    pp_mfma<0, 2>(acc, a, b1);
+    pp_barrier();
+    // ---- P2
+    pp_load_a(a, st + 1 * 16384, ra, fr, fg);
+    if (n2) pp2_issue<0>(smem, src, wave, kt + 2, kt & 1);
+    pp_barrier();
+    pp_mfma<4, 2>(acc, a, b1);
+    pp_barrier();
+    // ---- P3
+    if (n2) {
+      pp2_issue<2>(smem, src, wave, kt + 2, kt & 1);
+      pp2_issue<3>(smem, src, wave, kt + 2, kt & 1);
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    pp_barrier();
+    pp_mfma<4, 0>(acc, a, b0);
+    pp_barrier();
+  }
+  if (wm == 0) pp_barrier();                 // re-align
+}
+
+template <int EPI>
+__global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
+    int M, int N, int K, const bf16_t* __restrict__ A, int lda,
+    const bf16_t* __restrict__ Bt, int ldb, int tiles_m, int tiles_n, EpiArgs e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tm = tile / tiles_n, tn = tile - (tile / tiles_n) * tiles_n;
+  const int m0 = tm * BBM, n0 = tn * BBN;
+  PP2Src src;
+  pp2_sources(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane);
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fg = lane >> 4;
+  pp2_mainloop(acc, smem, src, K / 64, wave, wm, wn, fr, fg);
+  float* ep = reinterpret_cast<float*>(smem) + wave * 32 * 68;
+  const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
+  if constexpr (EPI != EPI_GENERIC) {
+    if (m0 + BBM <= M && n0 + BBN <= N) {
+      epilogue_fast<EPI>(acc, ep, lane, m_base, n_base, e);
+      return;
+    }
+  }
+  epilogue_generic(acc, ep, lane, M, N, m_base, n_base, e);
+}
+
 template <int EPI, bool kDiagSkipEpilogue>
 __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pingpong_kernel(
     int M, int N, int K, const bf16_t* __restrict__ A, int lda,
@@ -768,7 +911,9 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
           reinterpret_cast<const void*>(&gemm_tn_bf16_pingpong_kernel<EPI_GENERIC, false>),
           reinterpret_cast<const void*>(&gemm_tn_bf16_pingpong_kernel<4, true>),
           reinterpret_cast<const void*>(&gemm_tn_bf16_persistent_kernel<EPI_GENERIC>),
+          reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<EPI_GENERIC>),
 #define VTD_PP_FN(C) reinterpret_cast<const void*>(&gemm_tn_bf16_pingpong_kernel<C, false>), \
+                     reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C>), \
                      reinterpret_cast<const void*>(&gemm_tn_bf16_persistent_kernel<C>),
           VTD_PP_FN(0) VTD_PP_FN(1) VTD_PP_FN(2) VTD_PP_FN(4) VTD_PP_FN(5) VTD_PP_FN(6)
           VTD_PP_FN(8) VTD_PP_FN(9) VTD_PP_FN(10) VTD_PP_FN(12) VTD_PP_FN(13) VTD_PP_FN(14)
@@ -778,9 +923,11 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
       attr = true;
     }
+    // 6 = ping-pong v2 (default); 1 = ping-pong v1; 4 = persistent; 0 = 2-barrier;
+    // 2, 3, 5 = timing diagnostics (wrong outputs)
     static const int variant = [] {
       const char* v = getenv("VTD_GEMM_VARIANT");
-      return v ? atoi(v) : 1;
+      return v ? atoi(v) : 6;
     }();
     const dim3 g(tiles_m * tiles_n), b(BNT);
     const bf16_t* a16 = static_cast<const bf16_t*>(A);
@@ -809,12 +956,16 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
         return n;
       }();
       const bool persistent = variant == 4;
+      const bool pp2 = variant == 6;
       if (variant == 5) e.scatter_tokens = -2;      // diag: all tiles store to rows 0..255
       const dim3 gp(std::min(tiles_m * tiles_n, num_cu));
       switch (code) {
 #define VTD_PP_CASE(C)                                                                      \
   case C:                                                                                   \
-    if (persistent)                                                                         \
+    if (pp2)                                                                                \
+      hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C>), g, b, 2 * BSTAGE, stream, M, N, K,  \
+                         a16, lda, b16, ldb, tiles_m, tiles_n, e);                          \
+    else if (persistent)                                                                    \
       hipLaunchKernelGGL((gemm_tn_bf16_persistent_kernel<C>), gp, b, 2 * BSTAGE, stream, M, \
                          N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);                    \
     else                                                                                    \
@@ -827,7 +978,10 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
         VTD_PP_CASE(12) VTD_PP_CASE(13) VTD_PP_CASE(14)
 #undef VTD_PP_CASE
         default:
-          if (persistent)
+          if (pp2)
+            hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<EPI_GENERIC>), g, b, 2 * BSTAGE,
+                               stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);
+          else if (persistent)
             hipLaunchKernelGGL((gemm_tn_bf16_persistent_kernel<EPI_GENERIC>), gp, b,
                                2 * BSTAGE, stream, M, N, K, a16, lda, b16, ldb, tiles_m,
                                tiles_n, e);
