@@ -593,32 +593,45 @@ __device__ __forceinline__ int grp_tile_row(int g, int gr) {
                : (gr >> 5) * 64 + (g - 2) * 32 + (gr & 31);  // Y0 / Y1 (B rows)
 }
 
-struct PP2Src {   // per-lane DMA sources of this tile: [group][piece]
-  const char* p[4][2];
+// DMA source addressing of one tile, from wave-uniform scalars only (the per-lane part,
+// row-in-piece and swizzled chunk, is rederived from the lane id at each issue): keeps
+// 8 x 64-bit per-lane pointers out of the K loop's register budget.
+struct PP2Src {
+  const bf16_t* A; const bf16_t* Bt;
+  int lda, ldb, mlast, nlast, m0, n0;   // mlast = M - 1, nlast = N - 1
 };
 
 __device__ __forceinline__ void pp2_sources(PP2Src& src, const bf16_t* A, int lda, int M,
                                             const bf16_t* Bt, int ldb, int N, int m0, int n0,
-                                            int wave, int lane) {
-  const int prow = lane >> 3, pchunk = (lane & 7) ^ prow;
-#pragma unroll
-  for (int g = 0; g < 4; ++g)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int tr = grp_tile_row(g, (wave * 2 + j) * 8 + prow);
-      src.p[g][j] = g < 2
-          ? reinterpret_cast<const char*>(A + (int64_t)min(m0 + tr, M - 1) * lda) + pchunk * 16
-          : reinterpret_cast<const char*>(Bt + (int64_t)min(n0 + tr, N - 1) * ldb) + pchunk * 16;
-    }
+                                            int, int) {
+  src.A = A; src.Bt = Bt; src.lda = lda; src.ldb = ldb;
+  src.mlast = M - 1; src.nlast = N - 1; src.m0 = m0; src.n0 = n0;
+}
+
+__device__ __forceinline__ int opaque_lane() {
+  int l = __lane_id();
+  asm volatile("" : "+v"(l));
+  return l;
 }
 
 template <int G>
 __device__ __forceinline__ void pp2_issue(char* smem, const PP2Src& src, int wave, int kt,
                                           int stage) {
+  const int lane = opaque_lane();    // rederive per issue: no hoisted 64-bit pointers
+  const int prow = lane >> 3, pchunk = (lane & 7) ^ prow;
   char* dst = smem + stage * BSTAGE + G * 16384 + wave * 2 * 1024;
-  const int64_t ko = (int64_t)kt * KB;
-  glds16(src.p[G][0] + ko, dst);
-  glds16(src.p[G][1] + ko, dst + 1024);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int tr = grp_tile_row(G, (wave * 2 + j) * 8 + prow);
+    const char* g;
+    if constexpr (G < 2)
+      g = reinterpret_cast<const char*>(src.A + (int64_t)min(src.m0 + tr, src.mlast) * src.lda +
+                                        kt * 64) + pchunk * 16;
+    else
+      g = reinterpret_cast<const char*>(src.Bt + (int64_t)min(src.n0 + tr, src.nlast) * src.ldb +
+                                        kt * 64) + pchunk * 16;
+    glds16(g, dst + j * 1024);
+  }
 }
 
 __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, const PP2Src& src,
@@ -713,6 +726,236 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
     }
   }
   epilogue_generic(acc, ep, lane, M, N, m_base, n_base, e);
+}
+
+// ---------------------------------------------------------------------------------
+// Persistent pp2 ("pp2p"): LDS = stage 0 | stage 1 | 32 KiB epilogue region (160 KiB).
+// Per tile: K loop -> DMA of the NEXT tile's prologue (K-tiles 0 and 1) -> this tile's
+// epilogue through the private region -> next K loop.  The epilogue's S global stores
+// are younger than the next prologue's DMA, so the next loop's first waits add S to
+// their counts (vmcnt counts in issue order) and the stores drain under the first
+// ~1.5 K-tiles of compute instead of stalling the CU.
+// Epilogue region: per wave 16 rows x 64 floats (4 KiB), column XOR-swizzled by
+// ((row >> 2) & 3) << 4 so the accumulator writes of lanes 4 rows apart use different
+// bank halves; the 16-B row-vector reads keep 4 contiguous floats.
+constexpr int EPR_BYTES = 8 * 16 * 64 * 4;   // 32 KiB
+static_assert(2 * BSTAGE + EPR_BYTES <= 163840, "LDS budget");
+
+__device__ __forceinline__ int epx(int row, int col) {     // float index in a wave region
+  return row * 64 + (col ^ (((row >> 2) & 3) << 4));
+}
+
+template <int EPI>
+__device__ __forceinline__ void epilogue_fast_x(const f32x4 (&acc)[8][4], float* ep, int lane,
+                                                int m_base, int n_base, const EpiArgs& e) {
+  constexpr int ACT = EPI & 3;
+  constexpr bool OUT_BF16 = (EPI & 4) != 0;
+  constexpr bool RESID = (EPI & 8) != 0;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int c8 = (lane & 7) * 8, rsub = lane >> 3;
+  const f32x4 b0 = *reinterpret_cast<const f32x4*>(e.bias + n_base + c8);
+  const f32x4 b1 = *reinterpret_cast<const f32x4*>(e.bias + n_base + c8 + 4);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r2 = 0; r2 < 4; ++r2) ep[epx(fg * 4 + r2, j * 16 + fr)] = acc[p][j][r2];
+    f32x4 rv[2][2];
+    if constexpr (RESID) {
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const float* rp = e.resid + (int64_t)(m_base + p * 16 + it * 8 + rsub) * e.ldr + n_base + c8;
+        rv[it][0] = *reinterpret_cast<const f32x4*>(rp);
+        rv[it][1] = *reinterpret_cast<const f32x4*>(rp + 4);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int row = it * 8 + rsub;
+      f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + epx(row, c8)) + b0;
+      f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + epx(row, c8 + 4)) + b1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v0[j] = act_ct<ACT>(v0[j]);
+        v1[j] = act_ct<ACT>(v1[j]);
+      }
+      if constexpr (RESID) {
+        v0 += rv[it][0];
+        v1 += rv[it][1];
+      }
+      const int64_t idx = (int64_t)(m_base + p * 16 + row) * e.ldo + n_base + c8;
+      if constexpr (OUT_BF16) {
+        const i32x4 o = {(int)pack_bf16x2(v0[0], v0[1]), (int)pack_bf16x2(v0[2], v0[3]),
+                         (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
+        *reinterpret_cast<i32x4*>(static_cast<bf16_t*>(e.out) + idx) = o;
+      } else {
+        float* op = static_cast<float*>(e.out) + idx;
+        *reinterpret_cast<f32x4*>(op) = v0;
+        *reinterpret_cast<f32x4*>(op + 4) = v1;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void epilogue_generic_x(const f32x4 (&acc)[8][4], float* ep, int lane,
+                                                   int M, int N, int m_base, int n_base,
+                                                   const EpiArgs& e) {
+  const int fr = lane & 15, fg = lane >> 4;
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r2 = 0; r2 < 4; ++r2) ep[epx(fg * 4 + r2, j * 16 + fr)] = acc[p][j][r2];
+#pragma unroll 1
+    for (int it = 0; it < 4; ++it) {
+      const int row = it * 4 + (lane >> 4), col = (lane & 15) * 4;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(ep + epx(row, col));
+      epi_store4(e, M, N, m_base + p * 16 + row, n_base + col, v);
+    }
+  }
+}
+
+#define VTD_VMCNT(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+
+// K loop of pp2 without its prologue (K-tile 0 landed + barrier passed, K-tile 1's
+// X0/Y0/Y1 in flight).  kPost: S fast-epilogue stores sit between the prologue DMA and
+// this loop's DMA (see the comment above pp2p); waits that cover them add S.
+// Fragment loads that rederive their LDS addresses from an opaque copy of the lane id:
+// the compiler cannot hoist the 12 swizzled base addresses across the K loop, so they
+// do not compete with the accumulators for registers (a spill + reload there would add
+// a vmcnt(0) that drains the DMA and epilogue-store pipeline).
+__device__ __forceinline__ void pp_load_a_o(bf16x8 (&a)[4][2], const char* la, int row0) {
+  const int l = opaque_lane();
+  pp_load_a(a, la, row0, l & 15, l >> 4);
+}
+__device__ __forceinline__ void pp_load_b_o(bf16x8 (&b)[2][2], const char* lb, int row0) {
+  const int l = opaque_lane();
+  pp_load_b(b, lb, row0, l & 15, l >> 4);
+}
+
+template <int S>
+__device__ __forceinline__ void pp2_loop(f32x4 (&acc)[8][4], char* smem, const PP2Src& src,
+                                         int nk, int wave, int wm, int wn, int fr, int fg,
+                                         bool post) {
+  if (wm == 1) pp_barrier();
+  const int ra = wm * 64, rb = wn * 32;
+  bf16x8 a[4][2], b0[2][2], b1[2][2];
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* st = smem + (kt & 1) * BSTAGE;
+    const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+    const bool p0 = post && kt == 0, p01 = post && kt <= 1;
+    pp_load_a_o(a, st + 0 * 16384, ra);
+    pp_load_b_o(b0, st + 2 * 16384, rb);
+    if (n1) pp2_issue<1>(smem, src, wave, kt + 1, (kt + 1) & 1);
+    if (!n1) VTD_VMCNT(0);
+    else if (p01) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(10 + S) : "memory");
+    else VTD_VMCNT(10);
+    pp_barrier();
+    pp_mfma<0, 0>(acc, a, b0);
+    pp_barrier();
+    pp_load_b_o(b1, st + 3 * 16384, rb);
+    if (!n1) VTD_VMCNT(0);
+    else if (p0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + S) : "memory");
+    else VTD_VMCNT(8);
+    pp_barrier();
+    pp_mfma<0, 2>(acc, a, b1);
+    pp_barrier();
+    pp_load_a_o(a, st + 1 * 16384, ra);
+    if (n2) pp2_issue<0>(smem, src, wave, kt + 2, kt & 1);
+    pp_barrier();
+    pp_mfma<4, 2>(acc, a, b1);
+    pp_barrier();
+    if (n2) {
+      pp2_issue<2>(smem, src, wave, kt + 2, kt & 1);
+      pp2_issue<3>(smem, src, wave, kt + 2, kt & 1);
+      if (p0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(10 + S) : "memory");
+      else VTD_VMCNT(10);
+    } else {
+      VTD_VMCNT(0);
+    }
+    pp_barrier();
+    pp_mfma<4, 0>(acc, a, b0);
+    pp_barrier();
+  }
+  if (wm == 0) pp_barrier();
+}
+
+template <int EPI>
+__global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2p_kernel(
+    int M, int N, int K, const bf16_t* __restrict__ A, int lda,
+    const bf16_t* __restrict__ Bt, int ldb, int tiles_m, int tiles_n, EpiArgs e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int S = EPI < 0 ? 0 : epilogue_fast_stores<(EPI < 0 ? 0 : EPI), 16>();
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int nk = K / 64;
+  const int nwg = tiles_m * tiles_n;
+  const int q = nwg >> 3, r = nwg & 7;
+  float* ep = reinterpret_cast<float*>(smem + 2 * BSTAGE) + wave * 16 * 64;
+  int t = blockIdx.x;
+  if (t >= nwg) return;
+  auto origin = [&](int tt, int& m0, int& n0) {
+    const int x = tt & 7;
+    const int tile = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (tt >> 3);
+    const int tm = tile / tiles_n;
+    m0 = tm * BBM;
+    n0 = (tile - tm * tiles_n) * BBN;
+  };
+  auto prologue = [&](const PP2Src& src) {
+    pp2_issue<0>(smem, src, wave, 0, 0);
+    pp2_issue<2>(smem, src, wave, 0, 0);
+    pp2_issue<3>(smem, src, wave, 0, 0);
+    pp2_issue<1>(smem, src, wave, 0, 0);
+    if (nk > 1) {
+      pp2_issue<0>(smem, src, wave, 1, 1);
+      pp2_issue<2>(smem, src, wave, 1, 1);
+      pp2_issue<3>(smem, src, wave, 1, 1);
+    }
+  };
+  int m0, n0;
+  origin(t, m0, n0);
+  PP2Src src;
+  pp2_sources(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane);
+  prologue(src);
+  bool post = false;
+  for (;;) {
+    if (nk > 1) {
+      if (post) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 + S) : "memory");
+      else VTD_VMCNT(6);
+    } else {
+      if (post) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(S) : "memory");
+      else VTD_VMCNT(0);
+    }
+    pp_barrier();
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    pp2_loop<S>(acc, smem, src, nk, wave, wm, wn, fr, fg, post);
+    const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
+    const bool full = m0 + BBM <= M && n0 + BBN <= N;
+    const int tn = t + gridDim.x;
+    if (tn < nwg) {                          // next tile's prologue before this epilogue
+      origin(tn, m0, n0);
+      pp2_sources(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane);
+      prologue(src);
+    }
+    if (EPI != EPI_GENERIC && full) {
+      epilogue_fast_x<(EPI < 0 ? 0 : EPI)>(acc, ep, lane, m_base, n_base, e);
+      post = true;
+    } else {
+      epilogue_generic_x(acc, ep, lane, M, N, m_base, n_base, e);
+      post = false;
+    }
+    if (tn >= nwg) break;
+    t = tn;
+  }
 }
 
 template <int EPI, bool kDiagSkipEpilogue>
@@ -912,7 +1155,9 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
           reinterpret_cast<const void*>(&gemm_tn_bf16_pingpong_kernel<4, true>),
           reinterpret_cast<const void*>(&gemm_tn_bf16_persistent_kernel<EPI_GENERIC>),
           reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<EPI_GENERIC>),
+          reinterpret_cast<const void*>(&gemm_tn_bf16_pp2p_kernel<EPI_GENERIC>),
 #define VTD_PP_FN(C) reinterpret_cast<const void*>(&gemm_tn_bf16_pingpong_kernel<C, false>), \
+                     reinterpret_cast<const void*>(&gemm_tn_bf16_pp2p_kernel<C>), \
                      reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C>), \
                      reinterpret_cast<const void*>(&gemm_tn_bf16_persistent_kernel<C>),
           VTD_PP_FN(0) VTD_PP_FN(1) VTD_PP_FN(2) VTD_PP_FN(4) VTD_PP_FN(5) VTD_PP_FN(6)
@@ -920,7 +1165,8 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
 #undef VTD_PP_FN
       };
       for (const void* f : fns)
-        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  2 * BSTAGE + EPR_BYTES);
       attr = true;
     }
     // 6 = ping-pong v2 (default); 1 = ping-pong v1; 4 = persistent; 0 = 2-barrier;
@@ -957,12 +1203,16 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
       }();
       const bool persistent = variant == 4;
       const bool pp2 = variant == 6;
+      const bool pp2p = variant == 7;
       if (variant == 5) e.scatter_tokens = -2;      // diag: all tiles store to rows 0..255
       const dim3 gp(std::min(tiles_m * tiles_n, num_cu));
       switch (code) {
 #define VTD_PP_CASE(C)                                                                      \
   case C:                                                                                   \
-    if (pp2)                                                                                \
+    if (pp2p)                                                                               \
+      hipLaunchKernelGGL((gemm_tn_bf16_pp2p_kernel<C>), gp, b, 2 * BSTAGE + EPR_BYTES,      \
+                         stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);         \
+    else if (pp2)                                                                           \
       hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C>), g, b, 2 * BSTAGE, stream, M, N, K,  \
                          a16, lda, b16, ldb, tiles_m, tiles_n, e);                          \
     else if (persistent)                                                                    \
@@ -978,7 +1228,11 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
         VTD_PP_CASE(12) VTD_PP_CASE(13) VTD_PP_CASE(14)
 #undef VTD_PP_CASE
         default:
-          if (pp2)
+          if (pp2p)
+            hipLaunchKernelGGL((gemm_tn_bf16_pp2p_kernel<EPI_GENERIC>), gp, b,
+                               2 * BSTAGE + EPR_BYTES, stream, M, N, K, a16, lda, b16, ldb,
+                               tiles_m, tiles_n, e);
+          else if (pp2)
             hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<EPI_GENERIC>), g, b, 2 * BSTAGE,
                                stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);
           else if (persistent)
