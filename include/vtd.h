@@ -179,6 +179,16 @@ int vtd_attention(const void* qkv_dev, int B, int N, int heads, int dkp, int ldq
  * [sigmoid, sigmoid*79, clip(sigmoid)*608 x4]. */
 int vtd_decode(const float* logits_dev, int64_t n, float* dets_dev, void* stream);
 
+/* transform_predictions + the detection test of MeanAveragePrecision.update_state
+ * (vtd.py:1359-1384), per slot: dets as vtd_decode; category = round-half-even of the
+ * decoded class (tf.round); class confidence = (0.5 - |cls - category|) / 0.5;
+ * valid = objectness > obj_threshold && confidence > cls_threshold
+ * (Constants.OBJECTNESS_THRESHOLD / CLASSIFICATION_CONFIDENCE_THRESHOLD = 0.5).
+ * category_dev (int32) and valid_dev (uint8) may be NULL. */
+int vtd_decode_detections(const float* logits_dev, int64_t n, float* dets_dev,
+                          int32_t* category_dev, uint8_t* valid_dev, float obj_threshold,
+                          float cls_threshold, void* stream);
+
 /* ---------------------------------------------------------------- forward ------ */
 /* model(images, training=False) (vtd.py:579-581, ipynb:836):
  * images NHWC fp32 [B][H][W][C] in [-1, 1] -> logits fp32 [B][17][6] (pre-sigmoid),

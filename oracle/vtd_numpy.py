@@ -282,3 +282,20 @@ def synthetic_images(batch, shape, seed=1, letterbox=False):
         img[:, :band] = -1.0
         img[:, h - band:] = -1.0
     return img
+
+
+OBJECTNESS_THRESHOLD = 0.5                   # vtd.py:41
+CLASSIFICATION_CONFIDENCE_THRESHOLD = 0.5    # vtd.py:43
+
+
+def detection_mask(decoded, obj_thr=OBJECTNESS_THRESHOLD,
+                   cls_thr=CLASSIFICATION_CONFIDENCE_THRESHOLD):
+    """MeanAveragePrecision.update_state's prediction test (vtd.py:1359-1384) on the
+    output of transform_predictions: category = tf.round(class) (half to even, as
+    np.round), confidence = (0.5 - |class - category|) / 0.5, valid = objectness > 0.5
+    and confidence > 0.5.  Returns (category int32, valid bool)."""
+    d = np.asarray(decoded, dtype=np.float64)
+    cat = np.round(d[..., 1])
+    conf = (0.5 - np.abs(d[..., 1] - cat)) / 0.5
+    valid = (d[..., 0] > obj_thr) & (conf > cls_thr)
+    return cat.astype(np.int32), valid

@@ -290,3 +290,22 @@ def test_gemm_bf16_256_tile_path(L, cuda, M, N, K, act, out_dtype):
     err = np.abs(got - ref64) / np.maximum(np.abs(ref64), 1.0)
     bad = np.argwhere(err >= tol)
     assert err.max() < tol, (err.max(), len(bad), bad[:5].tolist())
+
+
+def test_decode_detections_matches_oracle(L, cuda):
+    """Fused decode + the MeanAveragePrecision prediction test (vtd.py:1359-1384)."""
+    from vision_transformer_detector_amd import decode_detections
+    g = np.random.default_rng(11)
+    logits = g.normal(0, 3, size=(64, 17, 6)).astype(np.float32)
+    dets, cat, valid = decode_detections(torch.from_numpy(logits).to(cuda))
+    exp = ref.transform_predictions(logits)
+    ecat, evalid = ref.detection_mask(exp)
+    assert np.abs(dets.cpu().numpy() - exp).max() < 1e-3
+    # ignore slots within float rounding of a threshold / a .5 class boundary
+    conf = (0.5 - np.abs(exp[..., 1] - np.round(exp[..., 1]))) / 0.5
+    frac = np.abs(exp[..., 1] - np.floor(exp[..., 1]) - 0.5)
+    safe = (np.abs(exp[..., 0] - 0.5) > 1e-4) & (np.abs(conf - 0.5) > 1e-4) & (frac > 1e-4)
+    assert safe.mean() > 0.95
+    np.testing.assert_array_equal(cat.cpu().numpy()[safe], ecat[safe])
+    np.testing.assert_array_equal(valid.cpu().numpy()[safe], evalid[safe])
+    assert 0 < evalid.sum() < evalid.size        # both outcomes exercised

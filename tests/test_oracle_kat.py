@@ -174,3 +174,14 @@ def test_seeded_inputs_are_platform_stable():
         assert _sha(x) == s["images_sha256"], name
         w = V.init_weights(seed=s["weight_seed"], perturb=s["perturb"], **kw)
         assert _sha(np.concatenate([v.ravel() for v in w.values()])) == s["weights_sha256"]
+
+
+def test_detection_mask_kat():
+    """vtd.py:1367-1384 on decoded predictions: tf.round is half-to-even; confidence
+    (0.5 - |c - round(c)|)/0.5 must exceed 0.5, i.e. |c - round(c)| < 0.25."""
+    d = np.zeros((1, 6, 6))
+    d[0, :, 0] = [0.9, 0.9, 0.9, 0.9, 0.5, 0.51]
+    d[0, :, 1] = [2.0, 2.5, 3.5, 2.24, 7.0, 7.2]
+    cat, valid = V.detection_mask(d)
+    np.testing.assert_array_equal(cat[0], [2, 2, 4, 2, 7, 7])
+    np.testing.assert_array_equal(valid[0], [True, False, False, True, False, True])

@@ -7,8 +7,9 @@ All arithmetic runs in hand-written gfx950 HIP kernels in `libvtd.so` (C-ABI:
 `include/vtd.h`); importing this package fails if that library is missing.
 """
 from .detector import (Constants, Model, create_vision_transformer_detector,  # noqa: F401
-                       keras_default_init, keras_weight_names, transform_predictions)
+                       decode_detections, detection_list, keras_default_init,
+                       keras_weight_names, transform_predictions)
 from . import presets  # noqa: F401
 
 __all__ = ["Constants", "Model", "create_vision_transformer_detector",
-           "transform_predictions", "presets"]
+           "transform_predictions", "decode_detections", "detection_list", "presets"]

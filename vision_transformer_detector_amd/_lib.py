@@ -90,6 +90,8 @@ SIGNATURES = {
     "vtd_attention": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_float,
                               c_void_p, c_int, c_int, c_void_p]),
     "vtd_decode": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
+    "vtd_decode_detections": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
+                                      c_float, c_float, c_void_p]),
     "vtd_forward": (c_int, [ctypes.POINTER(VtdConfig), ctypes.POINTER(VtdWeights), c_void_p,
                             c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "vtd_profile_enable": (c_int, [c_int]),

@@ -170,6 +170,28 @@ __global__ void decode_kernel(const float* __restrict__ logits, int64_t n,
   dets[i] = s * scale;
 }
 
+// transform_predictions + the thresholded detection test (vtd.py:1359-1384): one
+// thread per detection slot.  tf.round is round-half-to-even -> rintf.
+__global__ void decode_detections_kernel(const float* __restrict__ logits, int64_t n,
+                                         float* __restrict__ dets, int32_t* __restrict__ cat,
+                                         uint8_t* __restrict__ valid, float obj_thr,
+                                         float cls_thr) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float d[6];
+#pragma unroll
+  for (int f = 0; f < 6; ++f) {
+    float s = 1.f / (1.f + expf(-logits[i * 6 + f]));
+    if (f >= 2) s = fminf(fmaxf(s, 0.f), 1.f);
+    d[f] = s * (f == 0 ? 1.f : (f == 1 ? 79.f : 608.f));
+    if (dets) dets[i * 6 + f] = d[f];
+  }
+  const float c = rintf(d[1]);
+  const float conf = (0.5f - fabsf(d[1] - c)) / 0.5f;
+  if (cat) cat[i] = (int32_t)c;
+  if (valid) valid[i] = (d[0] > obj_thr && conf > cls_thr) ? 1 : 0;
+}
+
 // ------------------------------------------------------------------ packing
 template <typename TO>
 __global__ void pack_dense_kernel(const float* __restrict__ src, int K, int N, int kg,
@@ -255,6 +277,18 @@ int vtd_extract_patches(const float* images_dev, int B, int H, int W, int C, int
 
 int vtd_decode(const float* logits_dev, int64_t n, float* dets_dev, void* stream) {
   return vtd::decode_launch(logits_dev, n, dets_dev, static_cast<hipStream_t>(stream));
+}
+
+int vtd_decode_detections(const float* logits_dev, int64_t n, float* dets_dev,
+                          int32_t* category_dev, uint8_t* valid_dev, float obj_threshold,
+                          float cls_threshold, void* stream) {
+  VTD_CHECK_ARG(logits_dev && n > 0, "decode_detections: bad args");
+  vtd::ProfScope ps(static_cast<hipStream_t>(stream), vtd::PROF_OTHER, 0.0);
+  hipLaunchKernelGGL(vtd::decode_detections_kernel, dim3((unsigned)((n + 255) / 256)),
+                     dim3(256), 0, static_cast<hipStream_t>(stream), logits_dev, n, dets_dev,
+                     category_dev, valid_dev, obj_threshold, cls_threshold);
+  VTD_LAUNCH_CHECK("decode_detections");
+  return VTD_OK;
 }
 
 int vtd_pack_dense(const float* src_dev, int K, int N, int k_group, int k_group_p,

@@ -331,6 +331,15 @@ class Model:
         """(logits, transform_predictions(logits)) with the decode fused on device."""
         return self.forward(images, with_detections=True)
 
+    def detections(self, images, objectness_threshold: float = 0.5,
+                   classification_threshold: float = 0.5):
+        """Forward + transform_predictions + the prediction test MeanAveragePrecision
+        applies (vtd.py:1359-1384), fused on the device.  Returns (logits, dets,
+        category int32, valid bool), all (B, 17[, 6]) device tensors."""
+        logits = self.forward(images)
+        return (logits,) + decode_detections(logits, objectness_threshold,
+                                             classification_threshold)
+
     def predict(self, x, batch_size: int = 32, verbose=0):
         """keras.Model.predict: numpy in, numpy (N, 17, 6) logits out, batches of 32."""
         x = np.asarray(x, dtype=np.float32)
@@ -401,4 +410,46 @@ def transform_predictions(inputs):
         with torch.cuda.device(src.device):
             L.check(L.lib.vtd_decode(src.data_ptr(), n, out.data_ptr(), L.stream_ptr()),
                     "vtd_decode")
+    return out
+
+
+def decode_detections(logits, objectness_threshold: float = 0.5,
+                      classification_threshold: float = 0.5):
+    """Device-side transform_predictions + thresholded detection test (vtd.py:586-647,
+    1359-1384): category = round-half-even(class), confidence = (0.5 - |class -
+    category|) / 0.5, valid = objectness > thr and confidence > thr.
+    Returns (dets (..., 6) fp32, category (...) int32, valid (...) bool)."""
+    t = logits if torch.is_tensor(logits) else torch.as_tensor(np.asarray(logits))
+    if t.device.type != "cuda" or t.shape[-1] != 6:
+        raise ValueError("decode_detections needs a (..., 6) tensor on the HIP device")
+    src = t.to(torch.float32).contiguous()
+    n = src.numel() // 6
+    dets = torch.empty_like(src)
+    cat = torch.empty(src.shape[:-1], dtype=torch.int32, device=src.device)
+    valid = torch.empty(src.shape[:-1], dtype=torch.uint8, device=src.device)
+    if n:
+        with torch.cuda.device(src.device):
+            L.check(L.lib.vtd_decode_detections(src.data_ptr(), n, dets.data_ptr(),
+                                                cat.data_ptr(), valid.data_ptr(),
+                                                float(objectness_threshold),
+                                                float(classification_threshold),
+                                                L.stream_ptr()), "vtd_decode_detections")
+    return dets, cat, valid.bool()
+
+
+def detection_list(dets, category, valid):
+    """Host-side list per image of the valid detections:
+    [{"category": int, "objectness": float, "box_xywh": (cx, cy, w, h)}, ...]
+    (box fields in MODEL_IMAGE_SIZE pixels, as transform_predictions returns them:
+    [2] = cx, [3] = cy, [4] = height, [5] = width)."""
+    d, c, v = dets.cpu().numpy(), category.cpu().numpy(), valid.cpu().numpy()
+    out = []
+    for b in range(d.shape[0]):
+        items = []
+        for k in np.nonzero(v[b])[0]:
+            items.append({"slot": int(k), "category": int(c[b, k]),
+                          "objectness": float(d[b, k, 0]),
+                          "box_xywh": (float(d[b, k, 2]), float(d[b, k, 3]),
+                                       float(d[b, k, 5]), float(d[b, k, 4]))})
+        out.append(items)
     return out
