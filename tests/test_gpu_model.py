@@ -132,3 +132,16 @@ def test_hip_graph_capture_replays_forward(vtd, cuda):
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(logits_buf, eager)
+
+
+@pytest.mark.parametrize("ext", [".npz", ".safetensors"])
+def test_weight_file_round_trip(vtd, cuda, tmp_path, ext):
+    kw, w, x, logits, _ = load_tiny("tiny_mish")
+    m1 = vtd.create_vision_transformer_detector(**kw, dtype="float32")
+    m1.set_weights(w)
+    path = str(tmp_path / ("w" + ext))
+    m1.save_weights(path)
+    m2 = vtd.create_vision_transformer_detector(**kw, dtype="float32", seed=99)
+    m2.load_weights(path)
+    xb = torch.from_numpy(x).to(cuda)
+    assert torch.equal(m1(xb), m2(xb))

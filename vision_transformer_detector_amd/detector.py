@@ -200,6 +200,29 @@ class Model:
         self._master = master
         self._pack()
 
+    # ---- weight files (Keras-name keyed; see tools/keras_weights_to_npz.py)
+    def save_weights(self, path: str) -> None:
+        """Write the fp32 master weights keyed by Keras weight names to `.npz` or
+        `.safetensors` (the interchange format of this package)."""
+        d = {n: t.numpy() for n, t in self._master.items()}
+        if path.endswith(".safetensors"):
+            from safetensors.numpy import save_file
+            save_file(d, path)
+        else:
+            np.savez(path, **d)
+
+    def load_weights(self, path: str) -> None:
+        """Read weights written by save_weights or by tools/keras_weights_to_npz.py from
+        a reference Keras model (names may carry TF's ':0' suffix).  Only loaders that
+        execute nothing from the file are used (np.load allow_pickle=False, safetensors)."""
+        if path.endswith(".safetensors"):
+            from safetensors.numpy import load_file
+            raw = load_file(path)
+        else:
+            with np.load(path, allow_pickle=False) as z:
+                raw = {k: z[k] for k in z.files}
+        self.set_weights({k.split(":")[0]: v for k, v in raw.items()})
+
     def _pack(self):
         dims, dt = self.dims, self.dtype
         tdt = _TORCH_DTYPE[dt]
