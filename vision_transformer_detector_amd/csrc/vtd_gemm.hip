@@ -634,7 +634,49 @@ __device__ __forceinline__ void pp2_issue(char* smem, const PP2Src& src, int wav
   }
 }
 
-__device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, const PP2Src& src,
+// Buffer-resource DMA source (variant 8): one SRD per operand based at the tile's first
+// row; the 8 per-lane row offsets (clamped row * ld + swizzled chunk, bytes) are computed
+// once, and the K offset goes in the instruction's SGPR soffset, so an issue is
+// s_mov m0 + buffer_load_dwordx4 ... lds with no VALU address arithmetic.
+struct PP2BufSrc {
+  __amdgpu_buffer_rsrc_t ra, rb;
+  int off[4][2];
+};
+
+__device__ __forceinline__ void pp2b_sources(PP2BufSrc& s, const bf16_t* A, int lda, int M,
+                                             const bf16_t* Bt, int ldb, int N, int m0, int n0,
+                                             int wave, int lane) {
+  // records = bytes from the tile base to the end of the operand (clamped to 32 bits); all
+  // offsets are in range because rows are clamped to the last valid row.
+  const int64_t ra_bytes = (int64_t)(M - m0) * lda * 2, rb_bytes = (int64_t)(N - n0) * ldb * 2;
+  s.ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(A + (int64_t)m0 * lda), 0,
+                                           (int)std::min<int64_t>(ra_bytes, 0x7fffffff), 0x00020000);
+  s.rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(Bt + (int64_t)n0 * ldb), 0,
+                                           (int)std::min<int64_t>(rb_bytes, 0x7fffffff), 0x00020000);
+  const int prow = lane >> 3, pchunk = (lane & 7) ^ prow;
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int tr = grp_tile_row(g, (wave * 2 + j) * 8 + prow);
+      s.off[g][j] = g < 2 ? min(tr, M - 1 - m0) * lda * 2 + pchunk * 16
+                          : min(tr, N - 1 - n0) * ldb * 2 + pchunk * 16;
+    }
+}
+
+template <int G>
+__device__ __forceinline__ void pp2_issue(char* smem, const PP2BufSrc& src, int wave, int kt,
+                                          int stage) {
+  char* dst = smem + stage * BSTAGE + G * 16384 + wave * 2 * 1024;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(G < 2 ? src.ra : src.rb,
+                                             (lds_void_t*)(dst + j * 1024), 16, src.off[G][j],
+                                             kt * 128, 0, 0);
+}
+
+template <class Src>
+__device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, const Src& src,
                                              int nk, int wave, int wm, int wn, int fr, int fg) {
   // prologue: tile 0 complete, tile 1's X0/Y0/Y1 in flight
   pp2_issue<0>(smem, src, wave, 0, 0);
@@ -693,7 +735,7 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
   if (wm == 0) pp_barrier();                 // re-align
 }
 
-template <int EPI>
+template <int EPI, bool BUF = false>
 __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
     int M, int N, int K, const bf16_t* __restrict__ A, int lda,
     const bf16_t* __restrict__ Bt, int ldb, int tiles_m, int tiles_n, EpiArgs e) {
@@ -708,8 +750,12 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
   const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   const int tm = tile / tiles_n, tn = tile - (tile / tiles_n) * tiles_n;
   const int m0 = tm * BBM, n0 = tn * BBN;
-  PP2Src src;
-  pp2_sources(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane);
+  using Src = std::conditional_t<BUF, PP2BufSrc, PP2Src>;
+  Src src;
+  if constexpr (BUF)
+    pp2b_sources(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane);
+  else
+    pp2_sources(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane);
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -1156,9 +1202,11 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
           reinterpret_cast<const void*>(&gemm_tn_bf16_persistent_kernel<EPI_GENERIC>),
           reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<EPI_GENERIC>),
           reinterpret_cast<const void*>(&gemm_tn_bf16_pp2p_kernel<EPI_GENERIC>),
+          reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<EPI_GENERIC, true>),
 #define VTD_PP_FN(C) reinterpret_cast<const void*>(&gemm_tn_bf16_pingpong_kernel<C, false>), \
                      reinterpret_cast<const void*>(&gemm_tn_bf16_pp2p_kernel<C>), \
                      reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C>), \
+                     reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, true>), \
                      reinterpret_cast<const void*>(&gemm_tn_bf16_persistent_kernel<C>),
           VTD_PP_FN(0) VTD_PP_FN(1) VTD_PP_FN(2) VTD_PP_FN(4) VTD_PP_FN(5) VTD_PP_FN(6)
           VTD_PP_FN(8) VTD_PP_FN(9) VTD_PP_FN(10) VTD_PP_FN(12) VTD_PP_FN(13) VTD_PP_FN(14)
@@ -1169,11 +1217,12 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
                                   2 * BSTAGE + EPR_BYTES);
       attr = true;
     }
-    // 6 = ping-pong v2 (default); 1 = ping-pong v1; 4 = persistent; 0 = 2-barrier;
+    // 8 = ping-pong v2 with buffer-resource DMA (default); 6 = same with global_load_lds;
+    // 7 = persistent v2; 1 = ping-pong v1; 4 = persistent; 0 = 2-barrier;
     // 2, 3, 5 = timing diagnostics (wrong outputs)
     static const int variant = [] {
       const char* v = getenv("VTD_GEMM_VARIANT");
-      return v ? atoi(v) : 6;
+      return v ? atoi(v) : 8;
     }();
     const dim3 g(tiles_m * tiles_n), b(BNT);
     const bf16_t* a16 = static_cast<const bf16_t*>(A);
@@ -1204,6 +1253,7 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
       const bool persistent = variant == 4;
       const bool pp2 = variant == 6;
       const bool pp2p = variant == 7;
+      const bool pp2b = variant == 8;
       if (variant == 5) e.scatter_tokens = -2;      // diag: all tiles store to rows 0..255
       const dim3 gp(std::min(tiles_m * tiles_n, num_cu));
       switch (code) {
@@ -1212,6 +1262,9 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
     if (pp2p)                                                                               \
       hipLaunchKernelGGL((gemm_tn_bf16_pp2p_kernel<C>), gp, b, 2 * BSTAGE + EPR_BYTES,      \
                          stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);         \
+    else if (pp2b)                                                                          \
+      hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, true>), g, b, 2 * BSTAGE, stream, M,   \
+                         N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);                    \
     else if (pp2)                                                                           \
       hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C>), g, b, 2 * BSTAGE, stream, M, N, K,  \
                          a16, lda, b16, ldb, tiles_m, tiles_n, e);                          \
@@ -1232,6 +1285,9 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
             hipLaunchKernelGGL((gemm_tn_bf16_pp2p_kernel<EPI_GENERIC>), gp, b,
                                2 * BSTAGE + EPR_BYTES, stream, M, N, K, a16, lda, b16, ldb,
                                tiles_m, tiles_n, e);
+          else if (pp2b)
+            hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<EPI_GENERIC, true>), g, b, 2 * BSTAGE,
+                               stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);
           else if (pp2)
             hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<EPI_GENERIC>), g, b, 2 * BSTAGE,
                                stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);
