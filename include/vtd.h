@@ -197,6 +197,37 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
                 float* logits_dev, float* dets_dev, void* workspace_dev,
                 size_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------- metric ------- */
+/* iou_calculator (vtd.py:761-875), elementwise over n box pairs.  Each box is the last
+ * 4 floats (x, y, height, width) of a row of `stride` floats (stride 4: bare boxes;
+ * stride 6: detection rows).  iou_dev: n floats.  Intersections follow the reference's
+ * strict-inequality overlap test; IoU = inter / (union + 1e-8). */
+int vtd_iou(const float* label_bbox_dev, const float* pred_bbox_dev, int64_t n, int stride,
+            float* iou_dev, void* stream);
+
+/* MeanAveragePrecision (vtd.py:1268-2060).  The state is the reference's three
+ * Variables, caller-allocated in device memory:
+ *   latest_positive_bboxes    float [VTD_MAP_CLASSES][VTD_MAP_LATEST][VTD_MAP_PER_IMAGE][2]
+ *   labels_quantity_per_image float [VTD_MAP_CLASSES][VTD_MAP_LATEST]
+ *   showed_up_classes         uint8 [VTD_MAP_CLASSES]
+ * vtd_map_update = update_state(y_true, y_pred, use_transform_predictions=False)
+ * (vtd.py:1310-1862): y_true / y_pred fp32 [batch][boxes][6] rows (objectness, class,
+ * x, y, height, width); labels mark empty rows with class -8; y_pred is DECODED (run
+ * vtd_decode first for raw logits).  One launch per batch, stream-ordered.
+ * vtd_map_result = result() (vtd.py:1865-2049): out_dev fp32 [11] = the AP at IoU
+ * thresholds linspace(0.5, 0.95, 10), then the mAP (their mean). */
+#define VTD_MAP_CLASSES 80        /* Constants.CLASSES vtd.py:20 */
+#define VTD_MAP_LATEST 3          /* Constants.LATEST_RELATED_IMAGES vtd.py:32 */
+#define VTD_MAP_PER_IMAGE 14      /* Constants.BBOXES_PER_IMAGE vtd.py:37 */
+#define VTD_MAP_MAX_BOXES 64      /* boxes per image accepted by vtd_map_update */
+int vtd_map_reset(float* latest_positive_bboxes, float* labels_quantity_per_image,
+                  uint8_t* showed_up_classes, void* stream);
+int vtd_map_update(float* latest_positive_bboxes, float* labels_quantity_per_image,
+                   uint8_t* showed_up_classes, const float* y_true_dev,
+                   const float* y_pred_dev, int batch, int boxes, void* stream);
+int vtd_map_result(const float* latest_positive_bboxes, const float* labels_quantity_per_image,
+                   const uint8_t* showed_up_classes, float* out_dev, void* stream);
+
 /* Optional per-kernel timing of vtd_forward (hipEvents on `stream`, recorded around
  * every launch while enabled).  vtd_profile_read returns per-class totals in ms
  * summed over the forwards since the last reset; classes: 0 gemm, 1 attention,

@@ -9,7 +9,9 @@ All arithmetic runs in hand-written gfx950 HIP kernels in `libvtd.so` (C-ABI:
 from .detector import (Constants, Model, create_vision_transformer_detector,  # noqa: F401
                        decode_detections, detection_list, keras_default_init,
                        keras_weight_names, transform_predictions)
+from .metrics import MeanAveragePrecision, iou_calculator  # noqa: F401
 from . import presets  # noqa: F401
 
 __all__ = ["Constants", "Model", "create_vision_transformer_detector",
-           "transform_predictions", "decode_detections", "detection_list", "presets"]
+           "transform_predictions", "decode_detections", "detection_list", "presets",
+           "MeanAveragePrecision", "iou_calculator"]

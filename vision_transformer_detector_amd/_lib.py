@@ -20,6 +20,7 @@ MAX_MLP = 16
 MAX_HEAD = 64
 MAX_DETECT = 17
 PROF_CLASSES = 5
+MAP_CLASSES, MAP_LATEST, MAP_PER_IMAGE, MAP_MAX_BOXES = 80, 3, 14, 64
 
 F32, BF16 = 0, 1
 ACT_NONE, ACT_GELU_TANH, ACT_MISH = 0, 1, 2
@@ -92,6 +93,11 @@ SIGNATURES = {
     "vtd_decode": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "vtd_decode_detections": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                       c_float, c_float, c_void_p]),
+    "vtd_iou": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
+    "vtd_map_reset": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "vtd_map_update": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                               c_void_p]),
+    "vtd_map_result": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "vtd_forward": (c_int, [ctypes.POINTER(VtdConfig), ctypes.POINTER(VtdWeights), c_void_p,
                             c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "vtd_profile_enable": (c_int, [c_int]),

@@ -522,6 +522,44 @@ __device__ __forceinline__ void pp_load_b(bf16x8 (&b)[2][2], const char* lb, int
       b[j][s] = *reinterpret_cast<const bf16x8*>(lb + swz(row0 + j * 16 + fr, 4 * s + fg));
 }
 
+// ---- transposed-accumulator operand path (variant 9) -----------------------------------
+// MFMA operands swapped (D = B-tile x A-tile^T): a lane's 4 accumulator rows are 4
+// consecutive OUTPUT COLUMNS of one output row.  The B-group read is permuted so that
+// blocks j = 0 / 1 of a 32-column half hold columns 8*fg + 0..3 / 8*fg + 4..7: each lane
+// then owns 8 contiguous columns of a row and the epilogue stores 16 B per lane straight
+// from registers (no LDS staging).  The permuted read rows {0-3, 8-11, 16-19, 24-27} + 4j
+// would 2-way conflict under chunk ^ (row & 7); the B groups use
+// chunk ^ (row & 7) ^ ((row >> 2) & 4) instead (conflict-free for every ds_read_b128 lane
+// group of this pattern, checked exhaustively over the four wave offsets).
+__device__ __forceinline__ int swz_t(int row, int chunk) {
+  return row * KB + ((chunk ^ (row & 7) ^ ((row >> 2) & 4)) << 4);
+}
+__device__ __forceinline__ int perm_t(int j, int fr) { return 8 * (fr >> 2) + 4 * j + (fr & 3); }
+
+__device__ __forceinline__ void pp_load_b_t(bf16x8 (&b)[2][2], const char* lb, int row0, int fr,
+                                            int fg) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      b[j][s] = *reinterpret_cast<const bf16x8*>(lb + swz_t(row0 + perm_t(j, fr), 4 * s + fg));
+}
+
+template <int I0, int J0>
+__device__ __forceinline__ void pp_mfma_t(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][2],
+                                          const bf16x8 (&b)[2][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[I0 + i][J0 + j] =
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][s], a[i][s], acc[I0 + i][J0 + j], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+}
+
 // The ping-pong K loop.  Precondition: K-tile 0 is in stage 0 and visible to all waves
 // (its DMA drained and a workgroup barrier passed).  Postcondition: every wave has
 // finished every section (re-aligned), all DMA of this loop has landed.
@@ -643,6 +681,7 @@ struct PP2BufSrc {
   int off[4][2];
 };
 
+template <bool TR>
 __device__ __forceinline__ void pp2b_sources(PP2BufSrc& s, const bf16_t* A, int lda, int M,
                                              const bf16_t* Bt, int ldb, int N, int m0, int n0,
                                              int wave, int lane) {
@@ -659,8 +698,10 @@ __device__ __forceinline__ void pp2b_sources(PP2BufSrc& s, const bf16_t* A, int 
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int tr = grp_tile_row(g, (wave * 2 + j) * 8 + prow);
+      // transposed variant: B groups use swz_t (group row bit 4 = wave & 1 flips chunk bit 2)
+      const int bchunk = TR ? pchunk ^ ((wave & 1) << 2) : pchunk;
       s.off[g][j] = g < 2 ? min(tr, M - 1 - m0) * lda * 2 + pchunk * 16
-                          : min(tr, N - 1 - n0) * ldb * 2 + pchunk * 16;
+                          : min(tr, N - 1 - n0) * ldb * 2 + bchunk * 16;
     }
 }
 
@@ -675,7 +716,7 @@ __device__ __forceinline__ void pp2_issue(char* smem, const PP2BufSrc& src, int 
                                              kt * 128, 0, 0);
 }
 
-template <class Src>
+template <bool TR, class Src>
 __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, const Src& src,
                                              int nk, int wave, int wm, int wn, int fr, int fg) {
   // prologue: tile 0 complete, tile 1's X0/Y0/Y1 in flight
@@ -700,25 +741,30 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
     const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
     // ---- P0
     pp_load_a(a, st + 0 * 16384, ra, fr, fg);
-    pp_load_b(b0, st + 2 * 16384, rb, fr, fg);
+    if constexpr (TR) pp_load_b_t(b0, st + 2 * 16384, rb, fr, fg);
+    else pp_load_b(b0, st + 2 * 16384, rb, fr, fg);
     if (n1) pp2_issue<1>(smem, src, wave, kt + 1, (kt + 1) & 1);
     if (n1) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     pp_barrier();
-    pp_mfma<0, 0>(acc, a, b0);
+    if constexpr (TR) pp_mfma_t<0, 0>(acc, a, b0);
+    else pp_mfma<0, 0>(acc, a, b0);
     pp_barrier();
     // ---- P1
-    pp_load_b(b1, st + 3 * 16384, rb, fr, fg);
+    if constexpr (TR) pp_load_b_t(b1, st + 3 * 16384, rb, fr, fg);
+    else pp_load_b(b1, st + 3 * 16384, rb, fr, fg);
     if (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     pp_barrier();
-    pp_mfma<0, 2>(acc, a, b1);
+    if constexpr (TR) pp_mfma_t<0, 2>(acc, a, b1);
+    else pp_mfma<0, 2>(acc, a, b1);
     pp_barrier();
     // ---- P2
     pp_load_a(a, st + 1 * 16384, ra, fr, fg);
     if (n2) pp2_issue<0>(smem, src, wave, kt + 2, kt & 1);
     pp_barrier();
-    pp_mfma<4, 2>(acc, a, b1);
+    if constexpr (TR) pp_mfma_t<4, 2>(acc, a, b1);
+    else pp_mfma<4, 2>(acc, a, b1);
     pp_barrier();
     // ---- P3
     if (n2) {
@@ -729,13 +775,97 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     pp_barrier();
-    pp_mfma<4, 0>(acc, a, b0);
+    if constexpr (TR) pp_mfma_t<4, 0>(acc, a, b0);
+    else pp_mfma<4, 0>(acc, a, b0);
     pp_barrier();
   }
   if (wm == 0) pp_barrier();                 // re-align
 }
 
-template <int EPI, bool BUF = false>
+// Epilogue of the transposed variant, full tiles: lane (fr, fg) of wave (wm, wn) holds,
+// for accumulator row block i and column half jp, output row m_base + 16 i + fr and the 8
+// contiguous columns n_base + 32 jp + 8 fg + 0..7 (acc[i][2 jp] = first 4, acc[i][2 jp + 1]
+// = last 4).  Bias is loaded once; residual rows are fetched 4 row blocks at a time.
+template <int EPI>
+__device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int lane, int m_base,
+                                                int n_base, const EpiArgs& e) {
+  constexpr int ACT = EPI & 3;
+  constexpr bool OUT_BF16 = (EPI & 4) != 0;
+  constexpr bool RESID = (EPI & 8) != 0;
+  const int fr = lane & 15, fg = lane >> 4;
+  f32x4 bias[2][2];
+#pragma unroll
+  for (int jp = 0; jp < 2; ++jp)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      bias[jp][h] = *reinterpret_cast<const f32x4*>(e.bias + n_base + 32 * jp + 8 * fg + 4 * h);
+#pragma unroll
+  for (int i0 = 0; i0 < 8; i0 += 4) {
+    f32x4 rv[4][2][2];
+    if constexpr (RESID) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          const float* rp = e.resid + (int64_t)(m_base + 16 * (i0 + i) + fr) * e.ldr + n_base +
+                            32 * jp + 8 * fg;
+          rv[i][jp][0] = *reinterpret_cast<const f32x4*>(rp);
+          rv[i][jp][1] = *reinterpret_cast<const f32x4*>(rp + 4);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        f32x4 v0 = acc[i0 + i][2 * jp] + bias[jp][0];
+        f32x4 v1 = acc[i0 + i][2 * jp + 1] + bias[jp][1];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v0[r] = act_ct<ACT>(v0[r]);
+          v1[r] = act_ct<ACT>(v1[r]);
+        }
+        if constexpr (RESID) {
+          v0 += rv[i][jp][0];
+          v1 += rv[i][jp][1];
+        }
+        const int64_t idx =
+            (int64_t)(m_base + 16 * (i0 + i) + fr) * e.ldo + n_base + 32 * jp + 8 * fg;
+        if constexpr (OUT_BF16) {
+          const i32x4 o = {(int)pack_bf16x2(v0[0], v0[1]), (int)pack_bf16x2(v0[2], v0[3]),
+                           (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
+          *reinterpret_cast<i32x4*>(static_cast<bf16_t*>(e.out) + idx) = o;
+        } else {
+          float* op = static_cast<float*>(e.out) + idx;
+          *reinterpret_cast<f32x4*>(op) = v0;
+          *reinterpret_cast<f32x4*>(op + 4) = v1;
+        }
+      }
+  }
+}
+
+// Transposed variant, partial tiles and the runtime-flag modes: 32-row passes staged
+// through the wave's LDS region (a lane's 4 values are 4 contiguous columns: one 16-B
+// LDS store each), then the shared LDS -> global pass (bounds, rowadd, scatter, out2).
+// Staging keeps the accumulators in registers (32 inlined epi_store4 calls on registers
+// would not).
+__device__ __forceinline__ void epilogue_direct_generic(const f32x4 (&acc)[8][4], float* ep,
+                                                        int lane, int M, int N, int m_base,
+                                                        int n_base, const EpiArgs& e) {
+  constexpr int ES = 68;
+  const int fr = lane & 15, fg = lane >> 4;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        *reinterpret_cast<f32x4*>(ep + (i * 16 + fr) * ES + 32 * (jj >> 1) + 8 * fg +
+                                  4 * (jj & 1)) = acc[p * 2 + i][jj];
+    epilogue_generic_pass<32>(ep, lane, M, N, m_base + p * 32, n_base, e);
+  }
+}
+
+template <int EPI, bool BUF = false, bool TR = false>
 __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
     int M, int N, int K, const bf16_t* __restrict__ A, int lda,
     const bf16_t* __restrict__ Bt, int ldb, int tiles_m, int tiles_n, EpiArgs e) {
@@ -753,7 +883,7 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
   using Src = std::conditional_t<BUF, PP2BufSrc, PP2Src>;
   Src src;
   if constexpr (BUF)
-    pp2b_sources(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane);
+    pp2b_sources<TR>(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane);
   else
     pp2_sources(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane);
   f32x4 acc[8][4];
@@ -762,9 +892,20 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fg = lane >> 4;
-  pp2_mainloop(acc, smem, src, K / 64, wave, wm, wn, fr, fg);
-  float* ep = reinterpret_cast<float*>(smem) + wave * 32 * 68;
+  pp2_mainloop<TR>(acc, smem, src, K / 64, wave, wm, wn, fr, fg);
   const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
+  if constexpr (TR) {
+    if constexpr (EPI != EPI_GENERIC) {
+      if (m0 + BBM <= M && n0 + BBN <= N) {
+        epilogue_direct<EPI>(acc, lane, m_base, n_base, e);
+        return;
+      }
+    }
+    epilogue_direct_generic(acc, reinterpret_cast<float*>(smem) + wave * 32 * 68, lane, M, N,
+                            m_base, n_base, e);
+    return;
+  }
+  float* ep = reinterpret_cast<float*>(smem) + wave * 32 * 68;
   if constexpr (EPI != EPI_GENERIC) {
     if (m0 + BBM <= M && n0 + BBN <= N) {
       epilogue_fast<EPI>(acc, ep, lane, m_base, n_base, e);
@@ -1203,10 +1344,12 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
           reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<EPI_GENERIC>),
           reinterpret_cast<const void*>(&gemm_tn_bf16_pp2p_kernel<EPI_GENERIC>),
           reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<EPI_GENERIC, true>),
+          reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<EPI_GENERIC, true, true>),
 #define VTD_PP_FN(C) reinterpret_cast<const void*>(&gemm_tn_bf16_pingpong_kernel<C, false>), \
                      reinterpret_cast<const void*>(&gemm_tn_bf16_pp2p_kernel<C>), \
                      reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C>), \
                      reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, true>), \
+                     reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, true, true>), \
                      reinterpret_cast<const void*>(&gemm_tn_bf16_persistent_kernel<C>),
           VTD_PP_FN(0) VTD_PP_FN(1) VTD_PP_FN(2) VTD_PP_FN(4) VTD_PP_FN(5) VTD_PP_FN(6)
           VTD_PP_FN(8) VTD_PP_FN(9) VTD_PP_FN(10) VTD_PP_FN(12) VTD_PP_FN(13) VTD_PP_FN(14)
@@ -1217,12 +1360,14 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
                                   2 * BSTAGE + EPR_BYTES);
       attr = true;
     }
-    // 8 = ping-pong v2 with buffer-resource DMA (default); 6 = same with global_load_lds;
+    // 10 = auto (default): 9 when the epilogue has an activation, else 8
+    // 9 = 8 with transposed accumulators + register-direct epilogue;
+    // 8 = ping-pong v2 with buffer-resource DMA; 6 = same with global_load_lds;
     // 7 = persistent v2; 1 = ping-pong v1; 4 = persistent; 0 = 2-barrier;
     // 2, 3, 5 = timing diagnostics (wrong outputs)
     static const int variant = [] {
       const char* v = getenv("VTD_GEMM_VARIANT");
-      return v ? atoi(v) : 8;
+      return v ? atoi(v) : 10;
     }();
     const dim3 g(tiles_m * tiles_n), b(BNT);
     const bf16_t* a16 = static_cast<const bf16_t*>(A);
@@ -1253,7 +1398,10 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
       const bool persistent = variant == 4;
       const bool pp2 = variant == 6;
       const bool pp2p = variant == 7;
-      const bool pp2b = variant == 8;
+      // measured (gemm_bench, same box): 9 wins on activation epilogues (mlp1 -5 %,
+      // mlp2 -1.5 %), 8 on plain / f32+residual ones (attn_out -10 %, mlp3 -4 %)
+      const bool pp2t = variant == 9 || (variant == 10 && e.act != VTD_ACT_NONE);
+      const bool pp2b = variant == 8 || (variant == 10 && !pp2t);
       if (variant == 5) e.scatter_tokens = -2;      // diag: all tiles store to rows 0..255
       const dim3 gp(std::min(tiles_m * tiles_n, num_cu));
       switch (code) {
@@ -1265,6 +1413,9 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
     else if (pp2b)                                                                          \
       hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, true>), g, b, 2 * BSTAGE, stream, M,   \
                          N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);                    \
+    else if (pp2t)                                                                          \
+      hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, true, true>), g, b, 2 * BSTAGE, stream,\
+                         M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);                 \
     else if (pp2)                                                                           \
       hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C>), g, b, 2 * BSTAGE, stream, M, N, K,  \
                          a16, lda, b16, ldb, tiles_m, tiles_n, e);                          \
@@ -1288,6 +1439,10 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
           else if (pp2b)
             hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<EPI_GENERIC, true>), g, b, 2 * BSTAGE,
                                stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);
+          else if (pp2t)
+            hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<EPI_GENERIC, true, true>), g, b,
+                               2 * BSTAGE, stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n,
+                               e);
           else if (pp2)
             hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<EPI_GENERIC>), g, b, 2 * BSTAGE,
                                stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);
