@@ -269,10 +269,14 @@ def test_bad_args_raise_value_error(L, cuda):
 
 @pytest.mark.parametrize("M,N,K,act,out_dtype", [
     (4100, 2100, 192, 0, 0), (4100, 2100, 192, 1, 1), (8192, 1024, 64, 2, 0),
-    (3000, 3000, 320, 1, 1), (4352, 8704, 256, 1, 1)])
+    (3000, 3000, 320, 1, 1), (4352, 8704, 256, 1, 1), (4100, 2104, 192, 0, 0),
+    (2600, 776, 1536, 1, 1), (6272, 768, 768, 0, 0), (3000, 3000, 320, 2, 0),
+    (5000, 2304, 128, 0, 1), (3000, 1544, 3072, 1, 1), (6400, 2304, 2048, 0, 1),
+    (2100, 512, 4096, 2, 1)])
 def test_gemm_bf16_256_tile_path(L, cuda, M, N, K, act, out_dtype):
-    """Large problems (>= 128 tiles of 256 x 256) take the DMA-staged 256-tile kernel;
-    ragged M / N exercise the clamped loads and masked epilogue."""
+    """Large problems (>= 128 tiles of 256 x 256) take the DMA-staged 256-tile kernels
+    (pp2 in vtd_gemm.hip; the persistent pp3 for bf16-output layers with 2048 <= K <= 4096);
+    ragged M / N exercise the clamped / zero-filled loads and the masked epilogue."""
     g = torch.Generator(device=cuda).manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
     Bt = (torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)).to(torch.bfloat16)

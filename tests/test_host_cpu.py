@@ -177,3 +177,14 @@ def test_dropout_must_be_none():
     import vision_transformer_detector_amd as vtd
     with pytest.raises(ValueError):
         vtd.create_vision_transformer_detector(dropout=0.1)
+
+
+def test_pp3_lds_swizzle_conflict_free():
+    """The pp3 GEMM's 64-B-row LDS swizzle serves every ds_read_b128 lane group of its
+    plain and permuted fragment reads without bank conflicts (tools/swizzle_check.py)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "swizzle_check.py")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0 and "conflict-free" in r.stdout

@@ -1309,7 +1309,12 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_persistent_kernel(
   }
 }
 
+
 }  // namespace
+
+bool gemm_pp3_launch(int M, int N, int K, const bf16_t* A, int lda, const bf16_t* Bt,
+                     int ldb, const vtd_epilogue* epi, int code, int num_cu,
+                     hipStream_t stream);
 
 int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
                 int dtype, const vtd_epilogue* epi, hipStream_t stream, double flops) {
@@ -1404,6 +1409,15 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
       const bool pp2b = variant == 8 || (variant == 10 && !pp2t);
       if (variant == 5) e.scatter_tokens = -2;      // diag: all tiles store to rows 0..255
       const dim3 gp(std::min(tiles_m * tiles_n, num_cu));
+      // pp3 (vtd_gemm_pp3.hip, persistent, one DMA pipeline across tiles): opt-in
+      // variant 11.  Isolated it beats pp2 on long-K bf16 layers (mlp2 768 x 3072 -> 1536:
+      // 417 vs 463 us, operands L2/MALL-warm) but inside the forward, where A arrives from
+      // HBM, its 64-B-row DMA groups cost more than they save (15.3k vs 15.6k img/s).
+      if (variant == 11 && code != EPI_GENERIC &&
+          gemm_pp3_launch(M, N, K, a16, lda, b16, ldb, epi, code, num_cu, stream)) {
+        VTD_LAUNCH_CHECK("gemm");
+        return VTD_OK;
+      }
       switch (code) {
 #define VTD_PP_CASE(C)                                                                      \
   case C:                                                                                   \
