@@ -6,7 +6,7 @@ ModuleNotFoundError, no network), so the vectors come from the oracle restatemen
 they are generated.  Inputs and weights are regenerated from seeds (numpy PCG64 is
 platform-stable) for the large C1/C2 cases; tiny cases store everything explicitly.
 
-Run:  python tests/golden/make_golden.py
+Run:  python tests/golden/make_golden.py [seeded case names ...]
 """
 import hashlib
 import json
@@ -53,6 +53,10 @@ SEEDED = {
                                  encoder_num_heads=12, encoder_key_dim=64,
                                  encoder_repeat_times=12, encoder_mlp_quantities=3,
                                  use_mish=False), batch=1, wseed=0, iseed=1, letterbox=False),
+    # C3: ViT-B/16 preset at 640x640 (N = 1600 tokens: long-sequence attention)
+    "c3_vitb16_640_b1": dict(kw="vit_b16_640", batch=1, wseed=0, iseed=1, letterbox=True),
+    # C5: ViT-L/16 preset at 384x384 (D 1024, 16 heads, 24 layers)
+    "c5_vitl16_384_b1": dict(kw="vit_l16_384", batch=1, wseed=0, iseed=1, letterbox=True),
 }
 
 
@@ -60,8 +64,13 @@ def digest(a):
     return hashlib.sha256(np.ascontiguousarray(a, dtype=np.float32).tobytes()).hexdigest()
 
 
-def main():
+def main(only=None):
+    """only: names of SEEDED cases to (re)compute, merged into the existing JSON (the
+    tiny fixtures are then left untouched)."""
+    from vision_transformer_detector_amd import presets
     for name, c in TINY.items():
+        if only:
+            break
         kw = c["kw"]
         w = V.init_weights(seed=c["seed"], perturb=0.02, **kw)
         x = V.synthetic_images(c["batch"], V.resolve_kwargs(**kw)["input_shape"],
@@ -74,9 +83,12 @@ def main():
                             dets=V.transform_predictions(y),
                             kwargs=np.array(json.dumps(kw)), **arrays)
         print(name, y.shape, float(np.abs(y).max()))
-    seeded = {}
+    path = os.path.join(HERE, "seeded_forward.json")
+    seeded = json.load(open(path)) if only else {}
     for name, c in SEEDED.items():
-        kw = c["kw"]
+        if only and name not in only:
+            continue
+        kw = c["kw"] if isinstance(c["kw"], dict) else dict(presets.PRESETS[c["kw"]])
         shape = V.resolve_kwargs(**kw)["input_shape"]
         w = V.init_weights(seed=c["wseed"], perturb=0.02, **kw)
         x = V.synthetic_images(c["batch"], shape, seed=c["iseed"], letterbox=c["letterbox"])
@@ -90,12 +102,14 @@ def main():
                                 [v.ravel() for v in w.values()])),
                             logits=y.tolist())
         print(name, float(np.abs(y).max()))
-    with open(os.path.join(HERE, "seeded_forward.json"), "w") as f:
+    with open(path, "w") as f:
         json.dump(seeded, f, indent=1)
+    if only:
+        return
     shapes = V.layer_output_shapes()
     with open(os.path.join(HERE, "oracle_layer_shapes_c1.json"), "w") as f:
         json.dump({k: list(v) for k, v in shapes.items()}, f, indent=1)
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:] or None)

@@ -54,7 +54,8 @@ def test_tiny_golden(vtd, cuda, name, dtype):
 
 
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
-@pytest.mark.parametrize("case", ["c1_default_b1", "c2_vitb16_b1"])
+@pytest.mark.parametrize("case", ["c1_default_b1", "c2_vitb16_b1", "c3_vitb16_640_b1",
+                                  "c5_vitl16_384_b1"])
 def test_seeded_full_config(vtd, cuda, case, dtype):
     spec = json.load(open(os.path.join(GOLD, "seeded_forward.json")))[case]
     kw = dict(spec["kwargs"])
