@@ -319,63 +319,88 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
     if (active) {
       const char* kl = smem + (c & 1) * C::BUF;
       const char* vl = kl + C::KC * C::KS;
+      // 32-key blocks of this chunk holding at least one key (the last chunk may be
+      // ragged: N = 196 leaves 4 keys in it, one block)
+      const int nkb = min(2, (N - kv0 + 31) >> 5);
+      const bool ragged = kv0 + C::KC > N;
       f32x16 s[2];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
+        if (kb < nkb) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
-        const char* krow = kl + (kb * 32 + col) * C::KS;
+          for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+          const char* krow = kl + (kb * 32 + col) * C::KS;
 #pragma unroll
-        for (int st = 0; st < C::KSTEPS; ++st)
-          s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              *reinterpret_cast<const bf16x8*>(krow + (st * 16 + half * 8) * 2), qf[st], s[kb],
-              0, 0, 0);
+          for (int st = 0; st < C::KSTEPS; ++st)
+            s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                *reinterpret_cast<const bf16x8*>(krow + (st * 16 + half * 8) * 2), qf[st],
+                s[kb], 0, 0, 0);
+        }
+      }
+      // raw-score max; scores beyond N (ragged last chunk only) are -inf
+      if (ragged) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kv0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+            if (key >= N) s[kb][r] = -INFINITY;
+          }
       }
       float mx = -INFINITY;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
+        if (kb < nkb) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kv0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-          const float v = key < N ? s[kb][r] * scale_log2 : -INFINITY;
-          s[kb][r] = v;
-          mx = fmaxf(mx, v);
+          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
         }
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
-      const float m_new = fmaxf(m_run, mx);
-      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-      m_run = m_new;
+      mx = fmaxf(mx, __shfl_xor(mx, 32)) * scale_log2;
+      // deferred rescale (running max in log2 units): the accumulators are rescaled only
+      // when some lane's max grows by more than 8, so exp2 arguments stay <= 8 (P <= 256,
+      // exact in the bf16 P operand's range, l and O in fp32); the final 1/l normalises
+      // whatever max was used consistently for O and l
+      if (__builtin_amdgcn_ballot_w64(mx > m_run + 8.f)) {
+        const float m_new = fmaxf(m_run, mx);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        m_run = m_new;
+        l_run *= alpha;
+#pragma unroll
+        for (int i = 0; i < C::DB; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+      }
       float psum = 0.f;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
+        if (kb < nkb) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = __builtin_amdgcn_exp2f(s[kb][r] - m_new);
-          s[kb][r] = p;
-          psum += p;
+          for (int r = 0; r < 16; ++r) {
+            const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][r], scale_log2, -m_run));
+            s[kb][r] = p;
+            psum += p;
+          }
         }
-      l_run = l_run * alpha + psum;
-#pragma unroll
-      for (int i = 0; i < C::DB; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+      l_run += psum;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
+        if (kb < nkb) {
 #pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          const bf16x8 pb = __builtin_bit_cast(
-              bf16x8, i32x4{(int)pack_bf16x2(s[kb][8 * st + 0], s[kb][8 * st + 1]),
-                            (int)pack_bf16x2(s[kb][8 * st + 2], s[kb][8 * st + 3]),
-                            (int)pack_bf16x2(s[kb][8 * st + 4], s[kb][8 * st + 5]),
-                            (int)pack_bf16x2(s[kb][8 * st + 6], s[kb][8 * st + 7])});
-          const int key0 = kb * 32 + 16 * st + tr_key;
+          for (int st = 0; st < 2; ++st) {
+            const bf16x8 pb = __builtin_bit_cast(
+                bf16x8, i32x4{(int)pack_bf16x2(s[kb][8 * st + 0], s[kb][8 * st + 1]),
+                              (int)pack_bf16x2(s[kb][8 * st + 2], s[kb][8 * st + 3]),
+                              (int)pack_bf16x2(s[kb][8 * st + 4], s[kb][8 * st + 5]),
+                              (int)pack_bf16x2(s[kb][8 * st + 6], s[kb][8 * st + 7])});
+            const int key0 = kb * 32 + 16 * st + tr_key;
 #pragma unroll
-          for (int db = 0; db < C::DB; ++db) {
-            const char* va = vl + key0 * C::VS + (db * 32 + tr_d) * 2;
-            const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)va);
-            const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(va + 8 * C::VS));
-            const bf16x8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb, o[db], 0, 0, 0);
+            for (int db = 0; db < C::DB; ++db) {
+              const char* va = vl + key0 * C::VS + (db * 32 + tr_d) * 2;
+              const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)va);
+              const bf16x4 hi =
+                  __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(va + 8 * C::VS));
+              const bf16x8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+              o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb, o[db], 0, 0, 0);
+            }
           }
         }
     }
