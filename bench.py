@@ -1,7 +1,8 @@
 """Headline benchmark: images/s of the ViT-B/16 detector forward at batch 256 per GPU
 (BASELINE.json metric), bf16 operands / fp32 accumulate, synthetic COCO-shaped batches.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--dtype bf16|f32]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--dtype bf16|f32|fp8]
+                  [--preset vit_b16_224|vit_b16_640|vit_l16_384|c1]
   N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 One step = one forward of B images per rank (images already resident in HBM) + the
@@ -21,7 +22,8 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-PEAK_TFLOPS = {"bf16": 2516.6, "f32": 157.3}   # MI355X dense: 256 CU x 2.4 GHz (MICROARCH)
+PEAK_TFLOPS = {"bf16": 2516.6, "f32": 157.3,    # MI355X dense: 256 CU x 2.4 GHz (MICROARCH)
+               "fp8": 5033.2}                    # block-scaled MX-fp8 MFMA: 2x bf16 per clock
 HBM_PEAK_GBS = 8000.0
 
 
@@ -126,7 +128,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256, help="images per GPU")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32", "fp8"])
     ap.add_argument("--preset", default="vit_b16_224")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -145,7 +147,8 @@ def main():
     kw = dict(vtd.presets.PRESETS[args.preset])
     # identical weights on every rank (same seed): replicated-weight data parallelism
     model = vtd.create_vision_transformer_detector(
-        **kw, dtype="bfloat16" if args.dtype == "bf16" else "float32", device=dev, seed=0)
+        **kw, dtype={"bf16": "bfloat16", "f32": "float32", "fp8": "float8"}[args.dtype],
+        device=dev, seed=0)
     kw = {k: model.kwargs[k] for k in model.kwargs}
     shape = model.input_shape
     B = args.batch
@@ -226,7 +229,9 @@ def main():
                    "parallelism": f"dp{world}"},
         "mfma_util_attn_mlp": round(attn_mlp_fl * img_s / world / (peak * 1e12), 4),
         "model_tflops_per_gpu": round(total_fl * img_s / world / 1e12, 1),
-        "roofline": {"bound": "mfma", "kernel": "gemm_tn_bf16_* (all Dense layers)",
+        "roofline": {"bound": "mfma",
+                     "kernel": "gemm_mx8 (encoder Dense) + gemm_tn_bf16 (head)" if args.dtype == "fp8"
+                     else "gemm_tn_* (all Dense layers)",
                      "achieved": round(gemm_tf, 1) if gemm_tf else None, "peak": peak,
                      "unit": "TFLOP/s",
                      "frac": round(gemm_tf / peak, 4) if gemm_tf else None,

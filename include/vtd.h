@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define VTD_ABI_VERSION 1
+#define VTD_ABI_VERSION 2
 #define VTD_KALIGN 64          /* K / row padding granule, elements              */
 #define VTD_MAX_MLP 16         /* max encoder_mlp_quantities                     */
 #define VTD_MAX_HEAD 64        /* max mlp_head layers * repeats                   */
@@ -44,7 +44,10 @@ typedef enum vtd_status {
 
 typedef enum vtd_dtype {       /* compute (GEMM operand) dtype                   */
   VTD_F32 = 0,                 /* parity mode: f32 operands, f32 MFMA            */
-  VTD_BF16 = 1                 /* throughput mode: bf16 operands, f32 accumulate */
+  VTD_BF16 = 1,                /* throughput mode: bf16 operands, f32 accumulate */
+  VTD_FP8 = 2                  /* forward mode only (vtd_config.dtype): encoder  */
+                               /* Dense layers in MX-fp8 (vtd_gemm_mx8), the rest */
+                               /* as VTD_BF16                                     */
 } vtd_dtype;
 
 typedef enum vtd_act {         /* activation fused in a GEMM epilogue            */
@@ -93,13 +96,18 @@ typedef struct vtd_dims {
 
 /* Device pointers of one encoder block, packed by vtd_pack_dense / vtd_pack_vector.
  * Matrices: dtype = cfg.dtype, layout W^T [N_p][K_p] (row = output unit).
- * Vectors: fp32, padded with zeros. */
+ * Vectors: fp32, padded with zeros.
+ * VTD_FP8: w_qkv / w_out / w_mlp are MX-fp8 e4m3 [N_p][K8] (K8 = K_p rounded up to 128,
+ * vtd_quantize_mx8 of the packed fp32 matrix) and s_* their scales [K8/128][N_p][4];
+ * the s_* fields are ignored in the other modes. */
 typedef struct vtd_layer_weights {
   const float* ln1_gamma; const float* ln1_beta;        /* [d_p]                  */
   const void* w_qkv; const float* b_qkv;                /* [qkv_p][d_p], [qkv_p]  */
   const void* w_out; const float* b_out;                /* [d_p][inner_p], [d_p]  */
   const float* ln2_gamma; const float* ln2_beta;        /* [d_p]                  */
   const void* w_mlp[VTD_MAX_MLP]; const float* b_mlp[VTD_MAX_MLP];
+  const uint8_t* s_qkv; const uint8_t* s_out;          /* VTD_FP8 block scales   */
+  const uint8_t* s_mlp[VTD_MAX_MLP];
 } vtd_layer_weights;
 
 typedef struct vtd_weights {
@@ -160,6 +168,21 @@ typedef struct vtd_epilogue {
 } vtd_epilogue;
 int vtd_gemm(int M, int N, int K, const void* A_dev, int lda, const void* Bt_dev,
              int ldb, int dtype, const vtd_epilogue* epi, void* stream);
+
+/* MX-fp8 operands (OCP MX: e4m3 elements, one E8M0 scale byte e = 2^(e-127) per 32
+ * consecutive K elements).  vtd_quantize_mx8: x [rows][ldx] (x_dtype F32 or BF16), first
+ * K columns -> q [rows][ldq] e4m3 bytes with Kq columns (Kq % 128 == 0, columns [K, Kq)
+ * zero) and scales s[Kq/128][s_rows][4] (s_rows >= rows; the 4 scales of one 128-wide
+ * K-step of a row are one dword).  Block scale: the least 2^E with amax <= 448 * 2^E,
+ * E in [-126, 126]; elements round to nearest even (oracle/mx8.py restates both).
+ * vtd_gemm_mx8: as vtd_gemm (same epilogue) with A [M][lda], Bt [N][ldb] in that format,
+ * K % 128 == 0, lda/ldb % 16 == 0, sa_rows >= M, sb_rows >= N, both % 4 == 0;
+ * D = sum_k dec(A) dec(Bt) accumulated in fp32 by v_mfma_scale_f32_16x16x128_f8f6f4. */
+int vtd_quantize_mx8(const void* x_dev, int x_dtype, int64_t rows, int K, int ldx, int Kq,
+                     uint8_t* q_dev, int ldq, uint8_t* s_dev, int64_t s_rows, void* stream);
+int vtd_gemm_mx8(int M, int N, int K, const uint8_t* A_dev, int lda, const uint8_t* sA_dev,
+                 int64_t sa_rows, const uint8_t* Bt_dev, int ldb, const uint8_t* sB_dev,
+                 int64_t sb_rows, const vtd_epilogue* epi, void* stream);
 
 /* keras LayerNormalization(axis=-1, epsilon) (vtd.py:353-357, 375-379):
  * x fp32 [rows][ldx] -> y (dtype) [rows][ldy]; stats over the first D columns;

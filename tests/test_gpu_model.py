@@ -4,6 +4,8 @@ fp64 oracle golden vectors (tests/golden/, made by make_golden.py).
 Tolerances:
   float32 mode: |y - ref| <= 1e-3 |ref| + 1e-3 max|ref|   (north_star's 1e-3 rel-tol)
   bfloat16 mode: |y - ref| <= 3e-2 |ref| + 3e-2 max|ref|  (bf16 operands, fp32 accumulate)
+  float8 mode:   |y - ref| <= 1e-1 |ref| + 1e-1 max|ref|  (MX-fp8 e4m3 encoder Dense layers:
+                 3 mantissa bits per operand element, SURVEY.md §8d's stated fp8 bound)
 """
 import json
 import os
@@ -16,7 +18,7 @@ from oracle import vtd_numpy as V
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-TOL = {"float32": 1e-3, "bfloat16": 3e-2}
+TOL = {"float32": 1e-3, "bfloat16": 3e-2, "float8": 1e-1}
 
 
 def within(y, ref, tol):
@@ -40,7 +42,7 @@ def vtd(cuda):
     return m
 
 
-@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16", "float8"])
 @pytest.mark.parametrize("name", ["tiny_mish", "tiny_gelu", "tiny_seq400"])
 def test_tiny_golden(vtd, cuda, name, dtype):
     kw, w, x, logits, dets = load_tiny(name)
@@ -53,7 +55,7 @@ def test_tiny_golden(vtd, cuda, name, dtype):
         assert np.abs(d.cpu().numpy() - dets).max() < 1e-3 * 608
 
 
-@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16", "float8"])
 @pytest.mark.parametrize("case", ["c1_default_b1", "c2_vitb16_b1", "c3_vitb16_640_b1",
                                   "c5_vitl16_384_b1"])
 def test_seeded_full_config(vtd, cuda, case, dtype):

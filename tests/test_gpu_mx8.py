@@ -1,0 +1,96 @@
+"""MX-fp8 path of the VTD_FP8 mode on the GPU, through the C-ABI:
+  - vtd_quantize_mx8 against the CPU restatement oracle/mx8.py, element for element
+    (e4m3 values and E8M0 block exponents must be identical);
+  - vtd_gemm_mx8 against the fp64 product of the DEQUANTIZED device operands, so the
+    check isolates the block-scaled MFMA + fp32 accumulation + epilogue.  Tolerance
+    5e-4 relative for f32 outputs: the instruction reduces each 128-element K-step
+    inside the matrix core before the fp32 accumulate (measured max 1.1e-4 at K <= 1536,
+    6x the 2e-5 of the bf16 MFMA's exact fp32 fma chain); 8e-3 for bf16 outputs.
+"""
+import ctypes
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import mx8 as MX
+from oracle import vtd_numpy as ref
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def L(cuda):
+    from vision_transformer_detector_amd import _lib
+    return _lib
+
+
+def _quantize(L, x, Kq, s_rows=None):
+    rows, K = x.shape
+    s_rows = s_rows or -(-rows // 4) * 4
+    q = torch.full((rows, Kq), 0x7f, dtype=torch.uint8, device=x.device)
+    s = torch.full((Kq // 128 * s_rows * 4,), 0xff, dtype=torch.uint8, device=x.device)
+    dt = L.BF16 if x.dtype == torch.bfloat16 else L.F32
+    L.check(L.lib.vtd_quantize_mx8(x.data_ptr(), dt, rows, K, x.shape[1], Kq, q.data_ptr(),
+                                   Kq, s.data_ptr(), s_rows, L.stream_ptr()), "quantize_mx8")
+    torch.cuda.synchronize()
+    return q, s, s_rows
+
+
+@pytest.mark.parametrize("rows,K,Kq,src", [(64, 256, 256, "bf16"), (37, 200, 256, "bf16"),
+                                           (129, 768, 768, "f32"), (5, 96, 128, "f32")])
+def test_quantize_matches_oracle(L, cuda, rows, K, Kq, src):
+    g = torch.Generator(device=cuda).manual_seed(rows * K)
+    x = torch.randn(rows, K, generator=g, device=cuda)
+    # blocks spanning many binades: per-row magnitudes 2^-20 .. 2^20, one zero row
+    x = x * torch.exp2(torch.linspace(-20, 20, rows, device=cuda))[:, None]
+    x[rows // 2] = 0
+    x = x.to(torch.bfloat16) if src == "bf16" else x
+    q, s, s_rows = _quantize(L, x, Kq)
+    vals, E = MX.quantize(x.float().cpu().numpy(), Kq)
+    got = MX.decode_e4m3(q.cpu().numpy())
+    np.testing.assert_array_equal(got, vals)
+    s_np = s.cpu().numpy().reshape(Kq // 128, s_rows, 4)[:, :rows]
+    np.testing.assert_array_equal(s_np.transpose(1, 0, 2).reshape(rows, -1).astype(int) - 127, E)
+    deq = MX.dequantize(q.cpu().numpy(), s.cpu().numpy(), rows, Kq)
+    xf = np.zeros((rows, Kq))
+    xf[:, :K] = x.float().cpu().numpy()
+    # e4m3 relative step 2^-3 -> |err| <= 2^-4 |x| (normal range of the block)
+    blk = np.abs(xf).reshape(rows, -1, 32).max(axis=2, keepdims=True)
+    err = np.abs(deq - xf).reshape(rows, -1, 32)
+    assert np.all(err <= np.maximum(np.abs(xf.reshape(rows, -1, 32)) / 16, blk * 2.0 ** -9 + 1e-300))
+
+
+@pytest.mark.parametrize("M,N,K,act,out_dtype,resid", [
+    (300, 200, 256, 0, 0, False), (1000, 520, 384, 1, 1, False),
+    (4096, 1024, 1024, 1, 1, False), (2600, 776, 1536, 0, 0, True),
+    (513, 64, 128, 2, 0, False)])
+def test_gemm_mx8_matches_dequantized_fp64(L, cuda, M, N, K, act, out_dtype, resid):
+    g = torch.Generator(device=cuda).manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
+    W = torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)
+    qa, sa, sa_rows = _quantize(L, A, K)
+    qb, sb, sb_rows = _quantize(L, W, K)
+    bias = torch.randn(N, generator=g, device=cuda)
+    res = torch.randn(M, N, generator=g, device=cuda) if resid else None
+    out = torch.full((M, N), float("nan"), device=cuda,
+                     dtype=torch.float32 if out_dtype == 0 else torch.bfloat16)
+    e = L.VtdEpilogue()
+    e.bias, e.act = bias.data_ptr(), act
+    e.resid, e.ldr = (res.data_ptr(), N) if resid else (None, 0)
+    e.out, e.ldo, e.out_dtype = out.data_ptr(), N, out_dtype
+    L.check(L.lib.vtd_gemm_mx8(M, N, K, qa.data_ptr(), K, sa.data_ptr(), sa_rows, qb.data_ptr(),
+                               K, sb.data_ptr(), sb_rows, ctypes.byref(e), L.stream_ptr()),
+            "gemm_mx8")
+    torch.cuda.synchronize()
+    a64 = MX.dequantize(qa.cpu().numpy(), sa.cpu().numpy(), M, K)
+    b64 = MX.dequantize(qb.cpu().numpy(), sb.cpu().numpy(), N, K)
+    ref64 = a64 @ b64.T + bias.double().cpu().numpy()
+    ref64 = {0: lambda v: v, 1: ref.gelu_tanh, 2: ref.mish}[act](ref64)
+    if resid:
+        ref64 = ref64 + res.double().cpu().numpy()
+    got = out.double().cpu().numpy()
+    tol = 5e-4 if out_dtype == 0 else 8e-3
+    err = np.abs(got - ref64) / np.maximum(np.abs(ref64), 1.0)
+    assert err.max() < tol, (err.max(), np.argwhere(err >= tol)[:5].tolist())

@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede loading libvtd.so, see module doc)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvtd.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 KALIGN = 64
 MAX_MLP = 16
 MAX_HEAD = 64
@@ -22,7 +22,7 @@ MAX_DETECT = 17
 PROF_CLASSES = 5
 MAP_CLASSES, MAP_LATEST, MAP_PER_IMAGE, MAP_MAX_BOXES = 80, 3, 14, 64
 
-F32, BF16 = 0, 1
+F32, BF16, FP8 = 0, 1, 2
 ACT_NONE, ACT_GELU_TANH, ACT_MISH = 0, 1, 2
 STATUS = {0: "VTD_OK", -1: "VTD_ERR_INVALID_ARG", -2: "VTD_ERR_UNSUPPORTED",
           -3: "VTD_ERR_HIP", -4: "VTD_ERR_WORKSPACE"}
@@ -54,7 +54,8 @@ class VtdLayerWeights(ctypes.Structure):
         ("ln1_gamma", c_void_p), ("ln1_beta", c_void_p), ("w_qkv", c_void_p),
         ("b_qkv", c_void_p), ("w_out", c_void_p), ("b_out", c_void_p),
         ("ln2_gamma", c_void_p), ("ln2_beta", c_void_p),
-        ("w_mlp", c_void_p * MAX_MLP), ("b_mlp", c_void_p * MAX_MLP)]
+        ("w_mlp", c_void_p * MAX_MLP), ("b_mlp", c_void_p * MAX_MLP),
+        ("s_qkv", c_void_p), ("s_out", c_void_p), ("s_mlp", c_void_p * MAX_MLP)]
 
 
 class VtdWeights(ctypes.Structure):
@@ -86,6 +87,10 @@ SIGNATURES = {
                                     c_int, c_int, c_void_p]),
     "vtd_gemm": (c_int, [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int,
                          ctypes.POINTER(VtdEpilogue), c_void_p]),
+    "vtd_quantize_mx8": (c_int, [c_void_p, c_int, c_int64, c_int, c_int, c_int, c_void_p, c_int,
+                                 c_void_p, c_int64, c_void_p]),
+    "vtd_gemm_mx8": (c_int, [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int64, c_void_p,
+                             c_int, c_void_p, c_int64, ctypes.POINTER(VtdEpilogue), c_void_p]),
     "vtd_layernorm": (c_int, [c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_float,
                               c_void_p, c_int, c_int, c_void_p]),
     "vtd_attention": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_float,

@@ -1310,6 +1310,164 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_persistent_kernel(
 }
 
 
+
+// ============================================================================
+// MX-fp8 kernel (VTD_FP8 mode): A, Bt are OCP e4m3 bytes with one E8M0
+// scale per 32 K-elements (vtd_mx8.hip layout s[k / 128][rows][4]); D += A Bt^T via
+// v_mfma_scale_f32_16x16x128_f8f6f4 (block-scaled, twice the bf16 MFMA rate per clock).
+// Tile 256 x 256, K-step 128 elements = 128 B per row, so the operand staging is the
+// bf16 256 kernel's byte for byte (DMA 8 rows x 128 B per wave instruction); per stage
+// 1 KiB of A scales and 1 KiB of B scales follow (each wave DMAs 128 B of each: lanes 0-7).
+// Wave (wm, wn) computes 128 x 64 outputs = 8 x 4 blocks of 16 x 16.  Operand layout of
+// the instruction (measured, tools/mx8_probe.py): lane group g = lane / 16 supplies
+// K-elements [16 g, 16 g + 16) in its first 16 bytes and [64 + 16 g, 64 + 16 g + 16) in
+// its last 16, and its scale byte covers the 32-block [32 g, 32 g + 32) of the
+// instruction's K order.  So lane (fr, fg) reads 16-B chunks fg and fg + 4 of the row:
+// the instruction's block g is then exactly the quantizer's block g of the K-step and
+// the lane's scale is byte fg of the row's scale dword.  LDS chunk c of row r sits at
+// position c ^ (r & 7) (the bf16 kernels' image): conflict-free for both reads of every
+// ds_read_b128 lane group (exhaustive check in tools/swizzle_check.py).
+// Two barriers per K-step (the structure of gemm_tn_bf16_256_kernel).
+// ============================================================================
+constexpr int MX_SCALES = (BBM + BBN) * KB;   // scale blocks after the A and B tiles
+constexpr int MX_STAGE = MX_SCALES + 2048;     // 66 KiB per stage
+
+__device__ __forceinline__ int mx_swz(int row) { return row & 7; }
+
+__device__ __forceinline__ int mx_lds_scale(const char* p) {
+  return *reinterpret_cast<const int*>(p);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(BNT) void gemm_mx8_kernel(
+    int M, int N, int K, const uint8_t* __restrict__ A, int lda, const uint8_t* __restrict__ sA,
+    int64_t sa_rows, const uint8_t* __restrict__ Bt, int ldb, const uint8_t* __restrict__ sB,
+    int64_t sb_rows, int tiles_m, int tiles_n, EpiArgs e) {
+  typedef __attribute__((ext_vector_type(8))) int i32x8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tm = tile / tiles_n, tn = tile - (tile / tiles_n) * tiles_n;
+  const int m0 = tm * BBM, n0 = tn * BBN;
+
+  // operand DMA through buffer resources based at the tile's first row: wave fills tile
+  // rows wave*32 + 8 j + (lane >> 3), position lane & 7; one per-lane offset, the piece
+  // (j * 8 rows) and K-step in the scalar soffset; rows past M / N read as zero (range
+  // check).  Scales: lanes 0-7 of wave w copy the dwords of tile rows 32 w + 4 lane .. + 3.
+  const int prow = lane >> 3;
+  const int pchunk = (lane & 7) ^ mx_swz(prow);
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(A + (int64_t)m0 * lda), 0,
+      (int)std::min<int64_t>((int64_t)(M - m0) * lda, 0x7fffffff), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(Bt + (int64_t)n0 * ldb), 0,
+      (int)std::min<int64_t>((int64_t)(N - n0) * ldb, 0x7fffffff), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(sA), 0, (int)std::min<int64_t>(sa_rows * K / 32, 0x7fffffff), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(sB), 0, (int)std::min<int64_t>(sb_rows * K / 32, 0x7fffffff), 0x00020000);
+  const int voa = (wave * 32 + prow) * lda + pchunk * 16;
+  const int vob = (wave * 32 + prow) * ldb + pchunk * 16;
+  const int vsa = (m0 + wave * 32 + 4 * (lane & 7)) * 4;
+  const int vsb = (n0 + wave * 32 + 4 * (lane & 7)) * 4;
+  const int lds_piece = wave * 32 * KB;
+  auto issue = [&](int kt, int stage) {
+    char* base = smem + stage * MX_STAGE;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void_t*)(base + lds_piece + j * 8 * KB), 16,
+                                               voa, kt * KB + j * 8 * lda, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rb, (lds_void_t*)(base + BBM * KB + lds_piece + j * 8 * KB), 16, vob,
+          kt * KB + j * 8 * ldb, 0, 0);
+    if (lane < 8) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lds_void_t*)(base + MX_SCALES + wave * 128),
+                                               16, vsa, (int)(kt * sa_rows * 4), 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsb, (lds_void_t*)(base + MX_SCALES + 1024 + wave * 128), 16, vsb,
+          (int)(kt * sb_rows * 4), 0, 0);
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fg = lane >> 4;
+  // fragment row offsets: chunk positions 2 fg, 2 fg + 1 under the row's swizzle
+  const int sw = mx_swz(fr);
+  const int off0 = (fg ^ sw) * 16, off1 = ((fg + 4) ^ sw) * 16;
+  const char* pa0 = smem + (wm * 128 + fr) * KB + off0;
+  const char* pa1 = smem + (wm * 128 + fr) * KB + off1;
+  const char* pb0 = smem + BBM * KB + (wn * 64 + fr) * KB + off0;
+  const char* pb1 = smem + BBM * KB + (wn * 64 + fr) * KB + off1;
+  const char* psa = smem + MX_SCALES + (wm * 128 + fr) * 4;
+  const char* psb = smem + MX_SCALES + 1024 + (wn * 64 + fr) * 4;
+  const int nk = K / 128;
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // per-lane bases + immediate block offsets (16 rows = 2 KiB apart): no per-block
+    // address registers
+    const int so = (kt & 1) * MX_STAGE;
+    i32x8 bfr[4];
+    int sbv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const i32x4 lo = *reinterpret_cast<const i32x4*>(pb0 + so + j * 16 * KB);
+      const i32x4 hi = *reinterpret_cast<const i32x4*>(pb1 + so + j * 16 * KB);
+      bfr[j] = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      sbv[j] = mx_lds_scale(psb + so + j * 64) >> (8 * fg);
+    }
+#pragma unroll
+    for (int hs = 0; hs < 4; ++hs) {
+      i32x8 afr[2];
+      int sav[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int blk = 2 * hs + i;
+        const i32x4 lo = *reinterpret_cast<const i32x4*>(pa0 + so + blk * 16 * KB);
+        const i32x4 hi = *reinterpret_cast<const i32x4*>(pa1 + so + blk * 16 * KB);
+        afr[i] = i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        sav[i] = mx_lds_scale(psa + so + blk * 64) >> (8 * fg);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[2 * hs + i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              afr[i], bfr[j], acc[2 * hs + i][j], 0, 0, 0, sav[i], 0, sbv[j]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 2 < nk) issue(kt + 2, kt & 1);
+  }
+
+  float* ep = reinterpret_cast<float*>(smem) + wave * 32 * 68;
+  const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
+  if constexpr (EPI != EPI_GENERIC) {
+    if (m0 + BBM <= M && n0 + BBN <= N) {
+      epilogue_fast<EPI>(acc, ep, lane, m_base, n_base, e);
+      return;
+    }
+  }
+  epilogue_generic(acc, ep, lane, M, N, m_base, n_base, e);
+}
 }  // namespace
 
 bool gemm_pp3_launch(int M, int N, int K, const bf16_t* A, int lda, const bf16_t* Bt,
@@ -1482,6 +1640,63 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
   return VTD_OK;
 }
 
+
+int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_t* sA,
+                    int64_t sa_rows, const uint8_t* Bt, int ldb, const uint8_t* sB,
+                    int64_t sb_rows, const vtd_epilogue* epi, hipStream_t stream,
+                    double flops) {
+  VTD_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 128 == 0, "gemm_mx8: K must be a multiple of 128");
+  VTD_CHECK_ARG(A && Bt && sA && sB && epi && epi->out, "gemm_mx8: null pointer");
+  VTD_CHECK_ARG(lda >= K && ldb >= K && lda % 16 == 0 && ldb % 16 == 0,
+                "gemm_mx8: lda/ldb must be >= K and multiples of 16");
+  VTD_CHECK_ARG(sa_rows >= M && sb_rows >= N && sa_rows % 4 == 0 && sb_rows % 4 == 0,
+                "gemm_mx8: scale row counts must cover M / N and be multiples of 4");
+  VTD_CHECK_ARG(epi->out_dtype == VTD_F32 || epi->out_dtype == VTD_BF16, "gemm_mx8: bad out dtype");
+  VTD_CHECK_ARG(!epi->rowadd || epi->rowadd_period > 0, "gemm_mx8: rowadd_period");
+  VTD_CHECK_ARG(epi->scatter_tokens <= 0 || N <= VTD_MAX_DETECT,
+                "gemm_mx8: scatter epilogue needs N <= 17");
+  EpiArgs e{epi->bias, epi->rowadd, epi->rowadd_period,
+            epi->rowadd ? epi->rowadd_ncols : 0, epi->act, epi->resid, epi->ldr,
+            epi->out, epi->ldo, epi->out_dtype, epi->out2, epi->ldo2,
+            epi->scatter_tokens};
+  ProfScope ps(stream, PROF_GEMM, flops > 0 ? flops : 2.0 * M * N * (double)K);
+  const int tiles_m = (M + BBM - 1) / BBM, tiles_n = (N + BBN - 1) / BBN;
+  static bool attr = false;
+  if (!attr) {
+#define VTD_MX_FN(C) reinterpret_cast<const void*>(&gemm_mx8_kernel<C>),
+    const void* fns[] = {VTD_MX_FN(EPI_GENERIC) VTD_MX_FN(0) VTD_MX_FN(1) VTD_MX_FN(2)
+                         VTD_MX_FN(4) VTD_MX_FN(5) VTD_MX_FN(6) VTD_MX_FN(8) VTD_MX_FN(9)
+                         VTD_MX_FN(10) VTD_MX_FN(12) VTD_MX_FN(13) VTD_MX_FN(14)};
+#undef VTD_MX_FN
+    for (const void* f : fns)
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * MX_STAGE);
+    attr = true;
+  }
+  const bool fast = e.bias && !e.rowadd && e.scatter_tokens <= 0 && !e.out2 &&
+                    e.ldo % 8 == 0 && (!e.resid || e.ldr % 8 == 0) &&
+                    reinterpret_cast<uintptr_t>(e.out) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(e.bias) % 16 == 0 &&
+                    (!e.resid || reinterpret_cast<uintptr_t>(e.resid) % 16 == 0);
+  const int code = fast ? epi_code(e.act, e.out_dtype == VTD_BF16, e.resid != nullptr)
+                        : EPI_GENERIC;
+  const dim3 g(tiles_m * tiles_n), b(BNT);
+  switch (code) {
+#define VTD_MX_CASE(C)                                                                     \
+  case C:                                                                                  \
+    hipLaunchKernelGGL((gemm_mx8_kernel<C>), g, b, 2 * MX_STAGE, stream, M, N, K, A, lda,  \
+                       sA, sa_rows, Bt, ldb, sB, sb_rows, tiles_m, tiles_n, e);            \
+    break;
+    VTD_MX_CASE(0) VTD_MX_CASE(1) VTD_MX_CASE(2) VTD_MX_CASE(4) VTD_MX_CASE(5)
+    VTD_MX_CASE(6) VTD_MX_CASE(8) VTD_MX_CASE(9) VTD_MX_CASE(10) VTD_MX_CASE(12)
+    VTD_MX_CASE(13) VTD_MX_CASE(14)
+#undef VTD_MX_CASE
+    default:
+      hipLaunchKernelGGL((gemm_mx8_kernel<EPI_GENERIC>), g, b, 2 * MX_STAGE, stream, M, N, K,
+                         A, lda, sA, sa_rows, Bt, ldb, sB, sb_rows, tiles_m, tiles_n, e);
+  }
+  VTD_LAUNCH_CHECK("gemm_mx8");
+  return VTD_OK;
+}
 }  // namespace vtd
 
 extern "C" int vtd_gemm(int M, int N, int K, const void* A_dev, int lda,
@@ -1489,4 +1704,12 @@ extern "C" int vtd_gemm(int M, int N, int K, const void* A_dev, int lda,
                         void* stream) {
   return vtd::gemm_launch(M, N, K, A_dev, lda, Bt_dev, ldb, dtype, epi,
                           static_cast<hipStream_t>(stream), 0.0);
+}
+
+extern "C" int vtd_gemm_mx8(int M, int N, int K, const uint8_t* A_dev, int lda,
+                            const uint8_t* sA_dev, int64_t sa_rows, const uint8_t* Bt_dev,
+                            int ldb, const uint8_t* sB_dev, int64_t sb_rows,
+                            const vtd_epilogue* epi, void* stream) {
+  return vtd::gemm_mx8_launch(M, N, K, A_dev, lda, sA_dev, sa_rows, Bt_dev, ldb, sB_dev, sb_rows,
+                              epi, static_cast<hipStream_t>(stream), 0.0);
 }

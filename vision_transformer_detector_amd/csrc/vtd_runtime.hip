@@ -20,6 +20,12 @@ int layernorm_launch(const float* x, int64_t rows, int D, int ldx, const float* 
 int patches_launch(const float* img, int B, int H, int W, int C, int p, void* out, int ldo,
                    int dtype, hipStream_t st);
 int decode_launch(const float* logits, int64_t n, float* dets, hipStream_t st);
+int quantize_mx8_launch(const void* x, int x_dtype, int64_t rows, int K, int ldx, int Kq,
+                        uint8_t* q, int ldq, uint8_t* s, int64_t s_rows, hipStream_t st);
+int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_t* sA,
+                    int64_t sa_rows, const uint8_t* Bt, int ldb, const uint8_t* sB,
+                    int64_t sb_rows, const vtd_epilogue* epi, hipStream_t stream,
+                    double flops);
 
 // ------------------------------------------------------------------ errors
 static thread_local std::string g_last_error;
@@ -86,7 +92,8 @@ static int derive(const vtd_config* c, vtd_dims* d) {
   VTD_CHECK_ARG(c->head_last_units > 0 && c->head_layers > 0 && c->head_repeats > 0 &&
                     c->head_layers * c->head_repeats <= VTD_MAX_HEAD,
                 "bad mlp_head configuration");
-  VTD_CHECK_ARG(c->dtype == VTD_F32 || c->dtype == VTD_BF16, "dtype must be F32 or BF16");
+  VTD_CHECK_ARG(c->dtype == VTD_F32 || c->dtype == VTD_BF16 || c->dtype == VTD_FP8,
+                "dtype must be F32, BF16 or FP8");
   VTD_CHECK_ARG(c->key_dim <= 128, "encoder_key_dim > 128 not supported");
   const int p = c->patch_size;
   d->grid_h = (c->image_h + p - 1) / p;
@@ -130,9 +137,14 @@ static int derive(const vtd_config* c, vtd_dims* d) {
 
 namespace {
 struct Plan {
-  size_t patches, x, xb, h, qkv, attn, mlp0, mlp1, u, head0, head1, total;
+  size_t patches, x, xb, h, qkv, attn, mlp0, mlp1, u, head0, head1, q8, s8, total;
+  int k8_max;                       // widest MX-fp8 GEMM K (VTD_FP8)
+  int64_t s8_rows;                  // activation scale rows (rows rounded up to 4)
 };
-size_t es_of(int dtype) { return dtype == VTD_BF16 ? 2 : 4; }
+// activation / non-MX matrix dtype of a mode (VTD_FP8 keeps everything else in bf16)
+int act_dtype(int dtype) { return dtype == VTD_FP8 ? VTD_BF16 : dtype; }
+size_t es_of(int dtype) { return act_dtype(dtype) == VTD_BF16 ? 2 : 4; }
+int k8_of(int k) { return (int)round_up(k, 128); }
 Plan make_plan(const vtd_config* c, const vtd_dims& d) {
   Plan p{};
   size_t off = 0;
@@ -148,7 +160,7 @@ Plan make_plan(const vtd_config* c, const vtd_dims& d) {
   for (int j = 0; j < d.n_head; ++j) head_max = std::max(head_max, d.head_units_p[j]);
   p.patches = take(R * d.patch_dim_p * es);
   p.x = take(R * d.d_p * 4);
-  p.xb = take(c->dtype == VTD_BF16 ? R * d.d_p * 2 : 0);
+  p.xb = take(act_dtype(c->dtype) == VTD_BF16 ? R * d.d_p * 2 : 0);
   p.h = take(R * d.d_p * es);
   p.qkv = take(R * d.qkv_p * es);
   p.attn = take(R * d.inner_p * es);
@@ -157,6 +169,15 @@ Plan make_plan(const vtd_config* c, const vtd_dims& d) {
   p.u = take(HR * d.tokens_p * es);
   p.head0 = take(HR * head_max * es);
   p.head1 = take(HR * head_max * es);
+  // VTD_FP8: one MX-fp8 copy of the current encoder GEMM's A operand + its scales
+  p.k8_max = 0;
+  p.s8_rows = round_up((int64_t)R, 4);
+  if (c->dtype == VTD_FP8) {
+    p.k8_max = std::max(k8_of(d.d_p), k8_of(d.inner_p));
+    for (int j = 0; j + 1 < c->mlp_quantities; ++j) p.k8_max = std::max(p.k8_max, k8_of(d.mlp_units_p[j]));
+  }
+  p.q8 = take(R * p.k8_max);
+  p.s8 = take((size_t)p.s8_rows * p.k8_max / 32);
   p.total = off;
   return p;
 }
@@ -196,7 +217,8 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
                                        std::to_string(P.total) + " bytes)");
   hipStream_t st = static_cast<hipStream_t>(stream_);
   char* ws = static_cast<char*>(workspace);
-  const int dt = cfg->dtype;
+  const bool fp8 = cfg->dtype == VTD_FP8;
+  const int dt = act_dtype(cfg->dtype);
   const int B = cfg->batch, N = d.tokens, D = d.d, Dp = d.d_p;
   const int64_t R = d.rows;
   VTD_CHECK_ARG(R < (int64_t)1 << 31, "forward: batch*tokens too large");
@@ -212,6 +234,20 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
   void* head[2] = {ws + P.head0, ws + P.head1};
   const int act = cfg->use_mish ? VTD_ACT_MISH : VTD_ACT_GELU_TANH;
   const double fR = (double)R;
+  uint8_t* q8 = reinterpret_cast<uint8_t*>(ws + P.q8);
+  uint8_t* s8 = reinterpret_cast<uint8_t*>(ws + P.s8);
+  // encoder Dense layer (query/key/value, attention_output, MLP): bf16/f32 GEMM, or in
+  // VTD_FP8 mode MX-fp8 quantization of the bf16 A operand + the block-scaled MFMA GEMM
+  // against the MX-fp8 weights (W [Np][K8], S [K8/128][Np][4])
+  auto enc_gemm = [&](int Np, int K, const void* a, const void* W, const uint8_t* S,
+                      const vtd_epilogue* e, double flops) -> int {
+    if (!fp8) return gemm_launch(M, Np, K, a, K, W, K, dt, e, st, flops);
+    const int K8 = k8_of(K);
+    int r = quantize_mx8_launch(a, VTD_BF16, R, K, K, K8, q8, K8, s8, P.s8_rows, st);
+    if (r) return r;
+    return gemm_mx8_launch(M, Np, K8, q8, K8, s8, P.s8_rows, static_cast<const uint8_t*>(W), K8,
+                           S, Np, e, st, flops);
+  };
 
   // ---- ExtractImagePatches + flatten (vtd.py:271-280)
   rc = patches_launch(images, B, cfg->image_h, cfg->image_w, cfg->channels,
@@ -238,8 +274,8 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
       vtd_epilogue e{};
       e.bias = L.b_qkv; e.act = VTD_ACT_NONE;
       e.out = qkv; e.ldo = d.qkv_p; e.out_dtype = dt;
-      rc = gemm_launch(M, d.qkv_p, Dp, h, Dp, L.w_qkv, Dp, dt, &e, st,
-                       2.0 * fR * D * 3.0 * cfg->num_heads * cfg->key_dim);
+      rc = enc_gemm(d.qkv_p, Dp, h, L.w_qkv, L.s_qkv, &e,
+                    2.0 * fR * D * 3.0 * cfg->num_heads * cfg->key_dim);
       if (rc) return rc;
     }
     rc = attention_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale, attn,
@@ -251,8 +287,8 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
       e.bias = L.b_out; e.act = VTD_ACT_NONE;
       e.resid = x; e.ldr = Dp;
       e.out = x; e.ldo = Dp; e.out_dtype = VTD_F32;
-      rc = gemm_launch(M, Dp, d.inner_p, attn, d.inner_p, L.w_out, d.inner_p, dt, &e, st,
-                       2.0 * fR * cfg->num_heads * cfg->key_dim * D);
+      rc = enc_gemm(Dp, d.inner_p, attn, L.w_out, L.s_out, &e,
+                    2.0 * fR * cfg->num_heads * cfg->key_dim * D);
       if (rc) return rc;
     }
     rc = layernorm_launch(x, R, D, Dp, L.ln2_gamma, L.ln2_beta, 1e-3f, h, Dp, dt, st);
@@ -270,8 +306,8 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
       } else {
         e.out = mlp[j & 1]; e.ldo = d.mlp_units_p[j]; e.out_dtype = dt;
       }
-      rc = gemm_launch(M, d.mlp_units_p[j], k, a, k, L.w_mlp[j], k, dt, &e, st,
-                       2.0 * fR * kv * d.mlp_units[j]);
+      rc = enc_gemm(d.mlp_units_p[j], k, a, L.w_mlp[j], L.s_mlp[j], &e,
+                    2.0 * fR * kv * d.mlp_units[j]);
       if (rc) return rc;
       a = mlp[j & 1];
       k = d.mlp_units_p[j];

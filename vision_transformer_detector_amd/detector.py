@@ -37,8 +37,9 @@ class Constants(Enum):                                   # vtd.py:19-43
 
 
 _DTYPES = {"float32": L.F32, "fp32": L.F32, "f32": L.F32, "bfloat16": L.BF16,
-           "bf16": L.BF16}
-_TORCH_DTYPE = {L.F32: torch.float32, L.BF16: torch.bfloat16}
+           "bf16": L.BF16, "float8": L.FP8, "fp8": L.FP8, "mxfp8": L.FP8}
+# storage dtype of the activations and of the matrices outside the MX-fp8 layers
+_TORCH_DTYPE = {L.F32: torch.float32, L.BF16: torch.bfloat16, L.FP8: torch.bfloat16}
 
 
 def _resolve_dtype(dtype) -> int:
@@ -47,7 +48,8 @@ def _resolve_dtype(dtype) -> int:
     try:
         return _DTYPES[str(dtype).lower()]
     except KeyError:
-        raise ValueError(f"unsupported dtype {dtype!r}: use 'float32' (parity) or 'bfloat16'")
+        raise ValueError(f"unsupported dtype {dtype!r}: use 'float32' (parity), 'bfloat16' "
+                         "or 'float8' (MX-fp8 encoder Dense layers)")
 
 
 # ------------------------------------------------------------------------- names
@@ -224,7 +226,9 @@ class Model:
         self.set_weights({k.split(":")[0]: v for k, v in raw.items()})
 
     def _pack(self):
-        dims, dt = self.dims, self.dtype
+        dims = self.dims
+        fp8 = self.dtype == L.FP8
+        dt = L.BF16 if fp8 else self.dtype      # dtype of the non-MX matrices
         tdt = _TORCH_DTYPE[dt]
         dev = self.device
         keep, staging = [], []
@@ -240,16 +244,43 @@ class Model:
             staging.append(t)
             return t
 
-        def dense(name, rows_p, k_p, kg=None, kgp=None, ng=None, ngp=None, dst=None, off=0):
+        def dense(name, rows_p, k_p, kg=None, kgp=None, ng=None, ngp=None, dst=None, off=0,
+                  pdt=None):
             w = src(name + "/kernel")
             w2 = w.reshape(-1, w.shape[-1]) if w.dim() == 3 and kg is not None else w.reshape(w.shape[0], -1)
             K, N = w2.shape
             if dst is None:
                 dst = zeros(rows_p, k_p)
             L.check(L.lib.vtd_pack_dense(w2.data_ptr(), K, N, kg or K, kgp or K, ng or N,
-                                         ngp or N, dst.data_ptr(), k_p, off, dt, stream),
+                                         ngp or N, dst.data_ptr(), k_p, off,
+                                         dt if pdt is None else pdt, stream),
                     f"pack {name}")
             return dst
+
+        def f32_staging(rows_p, k_p):
+            t = torch.zeros((rows_p, k_p), dtype=torch.float32, device=dev)
+            staging.append(t)
+            return t
+
+        def mx8(w32, name):
+            """MX-fp8 copy of a packed fp32 matrix [rows_p][k_p]: e4m3 [rows_p][K8] and
+            scales [K8/128][rows_p][4] (vtd_quantize_mx8)."""
+            rows_p, k_p = w32.shape
+            k8 = -(-k_p // 128) * 128
+            q = zeros(rows_p, k8, dtype=torch.uint8)
+            sc = zeros(k8 // 128 * rows_p * 4, dtype=torch.uint8)
+            L.check(L.lib.vtd_quantize_mx8(w32.data_ptr(), L.F32, rows_p, k_p, k_p, k8,
+                                           q.data_ptr(), k8, sc.data_ptr(), rows_p, stream),
+                    f"quantize {name}")
+            return q.data_ptr(), sc.data_ptr()
+
+        def enc(name, rows_p, k_p, **kw):
+            """Encoder Dense layer: packed in the compute dtype, or MX-fp8 in FP8 mode.
+            Returns (matrix pointer, scale pointer or None)."""
+            if not fp8:
+                return dense(name, rows_p, k_p, **kw).data_ptr(), None
+            return mx8(dense(name, rows_p, k_p, dst=f32_staging(rows_p, k_p), pdt=L.F32, **kw),
+                       name)
 
         def vector(name, n_p, ng=None, ngp=None, dst=None, off=0):
             v = src(name).reshape(-1)
@@ -279,22 +310,24 @@ class Model:
             Ly.ln1_beta = vector(f"{ln1}/beta", dims.d_p).data_ptr()
             Ly.ln2_gamma = vector(f"{ln2}/gamma", dims.d_p).data_ptr()
             Ly.ln2_beta = vector(f"{ln2}/beta", dims.d_p).data_ptr()
-            wqkv = zeros(dims.qkv_p, dims.d_p)
+            wqkv = f32_staging(dims.qkv_p, dims.d_p) if fp8 else zeros(dims.qkv_p, dims.d_p)
             bqkv = zeros(dims.qkv_p, dtype=torch.float32)
             for part_i, part in enumerate(("query", "key", "value")):
                 off = part_i * dims.inner_p
                 # EinsumDense kernel (D, H, dk) -> (D, H*dk); columns padded per head
-                dense(f"{mha}/{part}", None, dims.d_p, ng=dk, ngp=dkp, dst=wqkv, off=off)
+                dense(f"{mha}/{part}", None, dims.d_p, ng=dk, ngp=dkp, dst=wqkv, off=off,
+                      pdt=L.F32 if fp8 else None)
                 vector(f"{mha}/{part}/bias", None, ng=dk, ngp=dkp, dst=bqkv, off=off)
-            Ly.w_qkv, Ly.b_qkv = wqkv.data_ptr(), bqkv.data_ptr()
+            Ly.w_qkv, Ly.s_qkv = mx8(wqkv, f"{mha}/qkv") if fp8 else (wqkv.data_ptr(), None)
+            Ly.b_qkv = bqkv.data_ptr()
             # attention_output kernel (H, dk, D) -> (H*dk, D); rows padded per head
-            Ly.w_out = dense(f"{mha}/attention_output", dims.d_p, dims.inner_p, kg=dk,
-                             kgp=dkp).data_ptr()
+            Ly.w_out, Ly.s_out = enc(f"{mha}/attention_output", dims.d_p, dims.inner_p, kg=dk,
+                                     kgp=dkp)
             Ly.b_out = vector(f"{mha}/attention_output/bias", dims.d_p).data_ptr()
             k_p = dims.d_p
             for j in range(kw["encoder_mlp_quantities"]):
                 n_p = dims.mlp_units_p[j]
-                Ly.w_mlp[j] = dense(f"MLP_{i}_{j + 1}", n_p, k_p).data_ptr()
+                Ly.w_mlp[j], Ly.s_mlp[j] = enc(f"MLP_{i}_{j + 1}", n_p, k_p)
                 Ly.b_mlp[j] = vector(f"MLP_{i}_{j + 1}/bias", n_p).data_ptr()
                 k_p = n_p
         W.layers = ctypes.cast(layers, ctypes.POINTER(L.VtdLayerWeights))
@@ -398,7 +431,9 @@ def create_vision_transformer_detector(
     forward path is inference-only); `max_weight`/`clip_weight` are weight constraints
     Keras applies only after optimizer steps (vtd.py:209-236), so they do not affect
     the forward and are accepted as no-ops.  Extra keyword-only options: `dtype`
-    ('bfloat16' throughput mode or 'float32' parity mode), `device`, `seed`."""
+    ('bfloat16' throughput mode, 'float32' parity mode, or 'float8': the encoder Dense
+    layers in MX-fp8 on the block-scaled fp8 MFMA, everything else bfloat16), `device`,
+    `seed`."""
     if dropout not in (None, 0, 0.0):
         raise ValueError("dropout must be None or 0 for the inference forward path")
     if input_shape is None:                                       # vtd.py:550-551
