@@ -313,3 +313,29 @@ def test_decode_detections_matches_oracle(L, cuda):
     np.testing.assert_array_equal(cat.cpu().numpy()[safe], ecat[safe])
     np.testing.assert_array_equal(valid.cpu().numpy()[safe], evalid[safe])
     assert 0 < evalid.sum() < evalid.size        # both outcomes exercised
+
+
+@pytest.mark.parametrize("act", [0, 1])
+def test_gemm_256_rowadd_out2_fast_path(L, cuda, act):
+    """The 256-tile kernels' fast epilogues with the two once-per-forward modes: the
+    position-embedding row add (vtd.py:305, columns < rowadd_ncols) and the bf16 copy
+    out2 of the last residual (the head's input)."""
+    M, N, K, T = 6272, 768, 768, 196
+    g = torch.Generator(device=cuda).manual_seed(17 + act)
+    A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
+    Bt = (torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g, device=cuda)
+    rowadd = torch.randn(T, generator=g, device=cuda)
+    resid = torch.randn(M, N, generator=g, device=cuda)
+    out = resid.clone()
+    out2 = torch.zeros(M, N, device=cuda, dtype=torch.bfloat16)
+    _gemm(L, A, Bt, L.BF16, bias=bias, rowadd=rowadd, rowadd_period=T, rowadd_ncols=700,
+          act=act, resid=out, out=out, out_dtype=0, out2=out2)
+    ref64 = (A.double() @ Bt.double().T + bias.double()).cpu().numpy()
+    ra = rowadd.double().cpu().numpy()[np.arange(M) % T]
+    ref64[:, :700] += ra[:, None]
+    ref64 = _np_act(act, ref64) + resid.double().cpu().numpy()
+    err = np.abs(out.double().cpu().numpy() - ref64) / np.maximum(np.abs(ref64), 1.0)
+    assert err.max() < 2e-5, err.max()
+    err2 = np.abs(out2.double().cpu().numpy() - ref64) / np.maximum(np.abs(ref64), 1.0)
+    assert err2.max() < 8e-3, err2.max()

@@ -185,3 +185,24 @@ def test_detection_mask_kat():
     cat, valid = V.detection_mask(d)
     np.testing.assert_array_equal(cat[0], [2, 2, 4, 2, 7, 7])
     np.testing.assert_array_equal(valid[0], [True, False, False, True, False, True])
+
+
+def test_mx8_format_kats():
+    """MX-fp8 restatement (oracle/mx8.py) against the OCP MX / e4m3 definitions: byte
+    decoding, round-to-nearest-even ties, the e4m3 range, and the block-scale rule."""
+    from oracle import mx8 as MX
+    dec = MX.decode_e4m3(np.array([0x7e, 0x38, 0x08, 0x01, 0x00, 0x80, 0xb8, 0x7f], np.uint8))
+    np.testing.assert_array_equal(dec[:7], [448.0, 1.0, 2.0 ** -6, 2.0 ** -9, 0.0, -0.0, -1.0])
+    assert np.isnan(dec[7])
+    # ties to even: 1.0625 is halfway between 1.0 (mantissa 0) and 1.125 (1) -> 1.0;
+    # 1.1875 halfway between 1.125 (1) and 1.25 (2) -> 1.25; subnormal 1.5 * 2^-9 -> 2^-8
+    np.testing.assert_array_equal(MX.round_e4m3([1.0625, 1.1875, 1.5 * 2.0 ** -9, 448.0, -3.3]),
+                                  [1.0, 1.25, 2.0 ** -8, 448.0, -3.25])
+    # least E with amax <= 448 * 2^E
+    np.testing.assert_array_equal(MX.block_exponent([448.0, 449.0, 56.0, 56.5, 0.0, 1e30]),
+                                  [0, 1, -3, -2, -126, 91])
+    x = np.random.default_rng(0).normal(size=(6, 100)) * np.exp2(np.arange(6) * 7 - 20)[:, None]
+    vals, E = MX.quantize(x, 128)
+    deq = (vals.reshape(6, 4, 32) * np.exp2(E)[..., None]).reshape(6, 128)[:, :100]
+    assert np.all(np.abs(deq - x) <= np.abs(x) / 16 + np.exp2(E.max(axis=1) - 10)[:, None])
+    assert np.all(np.abs(vals) <= 448)

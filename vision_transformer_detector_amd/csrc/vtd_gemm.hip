@@ -376,6 +376,25 @@ __device__ __forceinline__ float act_ct(float x) {
   else return x;
 }
 
+// Rare runtime modes kept on the fast epilogues (one launch per forward each): the
+// position-embedding row add of the patch embedding (vtd.py:305; before the activation,
+// columns < rowadd_ncols only) and the bf16 copy of the last encoder residual (out2, the
+// head's input).  8 contiguous columns n .. n + 7 of row m.
+__device__ __forceinline__ void epi_rowadd8(const EpiArgs& e, int m, int n, f32x4& v0,
+                                            f32x4& v1) {
+  const float ra = e.rowadd[m % e.rowadd_period];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v0[j] += (n + j < e.rowadd_ncols) ? ra : 0.f;
+    v1[j] += (n + 4 + j < e.rowadd_ncols) ? ra : 0.f;
+  }
+}
+__device__ __forceinline__ void epi_out2_8(const EpiArgs& e, int m, int n, f32x4 v0, f32x4 v1) {
+  const i32x4 o = {(int)pack_bf16x2(v0[0], v0[1]), (int)pack_bf16x2(v0[2], v0[3]),
+                   (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
+  *reinterpret_cast<i32x4*>(static_cast<bf16_t*>(e.out2) + (int64_t)m * e.ldo2 + n) = o;
+}
+
 // Writes the wave's 128 x 64 accumulator tile: 4 passes of 32 rows staged through the
 // wave's private LDS region; each lane then owns 8 consecutive columns of a row, so
 // residual reads and output writes are 16-B per lane (one 128-B line per 8 lanes).
@@ -417,6 +436,7 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
       const int row = it * 8 + rsub;
       f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + row * ES + c8) + b0;
       f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + row * ES + c8 + 4) + b1;
+      if (e.rowadd) epi_rowadd8(e, m_base + p * PR + row, n_base + c8, v0, v1);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         v0[j] = act_ct<ACT>(v0[j]);
@@ -426,6 +446,7 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
         v0 += rv[it][0];
         v1 += rv[it][1];
       }
+      if (e.out2) epi_out2_8(e, m_base + p * PR + row, n_base + c8, v0, v1);
       const int64_t idx = (int64_t)(m_base + p * PR + row) * e.ldo + n_base + c8;
       if constexpr (kDiagNoStore) {
         if (v0[0] != v0[0] && v1[3] != v1[3]) static_cast<float*>(e.out)[idx] = v0[1];
@@ -819,6 +840,8 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
       for (int jp = 0; jp < 2; ++jp) {
         f32x4 v0 = acc[i0 + i][2 * jp] + bias[jp][0];
         f32x4 v1 = acc[i0 + i][2 * jp + 1] + bias[jp][1];
+        const int mrow = m_base + 16 * (i0 + i) + fr, ncol = n_base + 32 * jp + 8 * fg;
+        if (e.rowadd) epi_rowadd8(e, mrow, ncol, v0, v1);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           v0[r] = act_ct<ACT>(v0[r]);
@@ -828,8 +851,8 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
           v0 += rv[i][jp][0];
           v1 += rv[i][jp][1];
         }
-        const int64_t idx =
-            (int64_t)(m_base + 16 * (i0 + i) + fr) * e.ldo + n_base + 32 * jp + 8 * fg;
+        if (e.out2) epi_out2_8(e, mrow, ncol, v0, v1);
+        const int64_t idx = (int64_t)mrow * e.ldo + ncol;
         if constexpr (OUT_BF16) {
           const i32x4 o = {(int)pack_bf16x2(v0[0], v0[1]), (int)pack_bf16x2(v0[2], v0[3]),
                            (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
@@ -1495,7 +1518,8 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
   const size_t lds = 4 * TILE_BYTES;
   ProfScope ps(stream, PROF_GEMM, flops > 0 ? flops : 2.0 * M * N * (double)K);
   const int tiles_m = (M + BBM - 1) / BBM, tiles_n = (N + BBN - 1) / BBN;
-  if (dtype == VTD_BF16 && tiles_m * tiles_n >= 128) {
+  // N <= 64 (the Dense(17) head projection): 128 x 128 tiles waste 8x less MFMA work
+  if (dtype == VTD_BF16 && tiles_m * tiles_n >= 128 && N > 64) {
     static bool attr = false;
     if (!attr) {
       const void* fns[] = {
@@ -1545,7 +1569,12 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
       hipLaunchKernelGGL((gemm_tn_bf16_pingpong_kernel<4, true>), g, b, 2 * BSTAGE,
                          stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);
     } else {
-      const bool fast = e.bias && !e.rowadd && (e.scatter_tokens <= 0 || variant == 5) && !e.out2 &&
+      // rowadd / out2 ride on the fast epilogues of every variant except the persistent
+      // pp2p (7) and pp3 (11), whose epilogues do not implement them
+      const bool rare_ok = variant != 7 && variant != 11 &&
+                           (!e.out2 || (e.ldo2 % 8 == 0 && reinterpret_cast<uintptr_t>(e.out2) % 16 == 0));
+      const bool fast = e.bias && (rare_ok || (!e.rowadd && !e.out2)) &&
+                        (e.scatter_tokens <= 0 || variant == 5) &&
                         e.ldo % 8 == 0 && (!e.resid || e.ldr % 8 == 0) &&
                         reinterpret_cast<uintptr_t>(e.out) % 16 == 0 &&
                         reinterpret_cast<uintptr_t>(e.bias) % 16 == 0 &&

@@ -399,6 +399,7 @@ bool gemm_pp3_launch(int M, int N, int K, const bf16_t* A, int lda, const bf16_t
                      int ldb, const vtd_epilogue* epi, int code, int num_cu,
                      hipStream_t stream) {
   if (N % 8 != 0 || N > P3_MAX_BIAS || K < 128 || K % 64 != 0 || !epi->bias) return false;
+  if (epi->rowadd || epi->out2 || epi->scatter_tokens > 0) return false;
   if ((int64_t)256 * std::max(lda, ldb) * 2 >= 0x7fffffff) return false;
   if (epi->ldo % 8 != 0 || (epi->resid && epi->ldr % 8 != 0)) return false;
   const int tiles_m = (M + BBM - 1) / BBM, tiles_n = (N + BBN - 1) / BBN;
