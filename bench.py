@@ -74,20 +74,21 @@ def traffic_per_launch():
         return None
 
 
-def gemm_alg_bytes(kw, dims, b):
+def gemm_alg_bytes(kw, dims, b, rb=2):
     """Algorithmic bytes of one forward's GEMMs (each operand read once, output written
-    once, residual read once), averaged per GEMM launch: the `traffic` yardstick."""
+    once, residual read once), averaged per GEMM launch: the `traffic` yardstick.
+    rb = bytes per residual-stream element (2: the bf16 stream of the bf16 / fp8 modes)."""
     rows, d = b * dims.tokens, kw["embedding_dim"]
     inner = kw["encoder_num_heads"] * kw["encoder_key_dim"]
-    g = [(rows, d, dims.patch_dim, 4, False)]
+    g = [(rows, d, dims.patch_dim, rb, False)]
     for _ in range(kw["encoder_repeat_times"]):
         g.append((rows, 3 * inner, d, 2, False))
-        g.append((rows, d, inner, 4, True))
+        g.append((rows, d, inner, rb, True))
         k = d
         for j in range(kw["encoder_mlp_quantities"]):
             n = dims.mlp_units[j]
             last = j == kw["encoder_mlp_quantities"] - 1
-            g.append((rows, n, k, 4 if last else 2, last))
+            g.append((rows, n, k, rb if last else 2, last))
             k = n
     g.append((rows, 17, d, 2, False))
     hr, k = b * 17, dims.tokens
@@ -95,7 +96,7 @@ def gemm_alg_bytes(kw, dims, b):
         g.append((hr, dims.head_units[j], k, 2, False))
         k = dims.head_units[j]
     g.append((hr, 6, k, 4, False))
-    tot = sum(2 * m * kk + 2 * n * kk + ob * m * n + (4 * m * n if r else 0)
+    tot = sum(2 * m * kk + 2 * n * kk + ob * m * n + (rb * m * n if r else 0)
               for m, n, kk, ob, r in g)
     return tot / len(g)
 
@@ -236,7 +237,9 @@ def main():
                      "unit": "TFLOP/s",
                      "frac": round(gemm_tf / peak, 4) if gemm_tf else None,
                      "traffic": traffic_per_launch(),
-                     "algorithmic_bytes_per_launch": round(gemm_alg_bytes(kw, model.dims, B)),
+                     "algorithmic_bytes_per_launch": round(gemm_alg_bytes(
+                         kw, model.dims, B, 4 if (args.dtype in ("f32", "float32") or
+                                              os.environ.get("VTD_RESID_F32", "0") != "0") else 2)),
                      "avg_launch_us": round(g["avg_us"], 2),
                      "launches_per_step": g["launches"] // max(1, args.steps)},
         "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv)

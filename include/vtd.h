@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define VTD_ABI_VERSION 2
+#define VTD_ABI_VERSION 3
 #define VTD_KALIGN 64          /* K / row padding granule, elements              */
 #define VTD_MAX_MLP 16         /* max encoder_mlp_quantities                     */
 #define VTD_MAX_HEAD 64        /* max mlp_head layers * repeats                   */
@@ -161,7 +161,7 @@ typedef struct vtd_epilogue {
   const float* rowadd;          /* position embedding per row, or NULL            */
   int rowadd_period, rowadd_ncols;
   int act;                      /* vtd_act                                         */
-  const float* resid; int ldr;  /* fp32 residual (may alias out), or NULL          */
+  const void* resid; int ldr;   /* residual in out_dtype (may alias out), or NULL  */
   void* out; int ldo; int out_dtype;
   void* out2; int ldo2;         /* optional bf16 copy                              */
   int scatter_tokens;
@@ -185,9 +185,9 @@ int vtd_gemm_mx8(int M, int N, int K, const uint8_t* A_dev, int lda, const uint8
                  int64_t sb_rows, const vtd_epilogue* epi, void* stream);
 
 /* keras LayerNormalization(axis=-1, epsilon) (vtd.py:353-357, 375-379):
- * x fp32 [rows][ldx] -> y (dtype) [rows][ldy]; stats over the first D columns;
- * columns [D, ldy) of y written as zero. */
-int vtd_layernorm(const float* x_dev, int64_t rows, int D, int ldx,
+ * x (x_dtype: fp32, or the bf16 residual stream) [rows][ldx] -> y (dtype) [rows][ldy];
+ * fp32 statistics over the first D columns; columns [D, ldy) of y written as zero. */
+int vtd_layernorm(const void* x_dev, int x_dtype, int64_t rows, int D, int ldx,
                   const float* gamma_dev, const float* beta_dev, float eps,
                   void* y_dev, int ldy, int dtype, void* stream);
 

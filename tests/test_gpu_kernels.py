@@ -134,19 +134,24 @@ def test_gemm_head_reshape_scatter(L, cuda, dtype, T):
     assert (out.cpu()[:, T:] == 0).all()
 
 
+@pytest.mark.parametrize("x_dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("D,ld", [(768, 768), (28, 64), (30, 64), (1024, 1024), (4100, 4160)])
-def test_layernorm(L, cuda, dtype, D, ld):
+def test_layernorm(L, cuda, dtype, x_dtype, D, ld):
+    """Input: the f32 residual stream, or the bf16 one of the bf16 / fp8 modes (the
+    expected value is computed from the bf16-rounded input)."""
     code, tdt = _dt(L, dtype)
+    xcode, xdt = _dt(L, x_dtype)
     rows = 37
     g = torch.Generator().manual_seed(D)
     x = torch.zeros(rows, ld)
     x[:, :D] = torch.randn(rows, D, generator=g) * 3 + 1
+    x = x.to(xdt).float()
     gamma = torch.zeros(ld); gamma[:D] = 1 + 0.1 * torch.randn(D, generator=g)
     beta = torch.zeros(ld); beta[:D] = 0.1 * torch.randn(D, generator=g)
     y = torch.full((rows, ld), float("nan"), dtype=tdt, device=cuda)
-    xd, gd, bd = x.to(cuda), gamma.to(cuda), beta.to(cuda)   # keep device copies alive
-    L.check(L.lib.vtd_layernorm(xd.data_ptr(), rows, D, ld, gd.data_ptr(), bd.data_ptr(),
+    xd, gd, bd = x.to(xdt).to(cuda), gamma.to(cuda), beta.to(cuda)   # keep device copies alive
+    L.check(L.lib.vtd_layernorm(xd.data_ptr(), xcode, rows, D, ld, gd.data_ptr(), bd.data_ptr(),
                                 1e-3, y.data_ptr(), ld, code, L.stream_ptr()), "ln")
     torch.cuda.synchronize()
     exp = ref.layer_norm(x[:, :D].double().numpy(), gamma[:D].double().numpy(),
@@ -164,7 +169,7 @@ def test_layernorm_epsilon_kat(L, cuda):
     y = torch.zeros(1, D, device=cuda)
     one, zero = torch.ones(D, device=cuda), torch.zeros(D, device=cuda)
     xd = x.to(cuda)
-    L.check(L.lib.vtd_layernorm(xd.data_ptr(), 1, D, D, one.data_ptr(),
+    L.check(L.lib.vtd_layernorm(xd.data_ptr(), L.F32, 1, D, D, one.data_ptr(),
                                 zero.data_ptr(), 1e-3, y.data_ptr(), D, L.F32, L.stream_ptr()))
     torch.cuda.synchronize()
     assert abs(y[0, 0].item() - math.sqrt(1e-3) / math.sqrt(2e-3)) < 1e-5
@@ -313,6 +318,25 @@ def test_decode_detections_matches_oracle(L, cuda):
     np.testing.assert_array_equal(cat.cpu().numpy()[safe], ecat[safe])
     np.testing.assert_array_equal(valid.cpu().numpy()[safe], evalid[safe])
     assert 0 < evalid.sum() < evalid.size        # both outcomes exercised
+
+
+@pytest.mark.parametrize("M,N,K,act", [
+    (6272, 768, 768, 0), (6272, 768, 1536, 1), (4100, 776, 768, 0), (4100, 776, 1536, 2),
+    (300, 200, 256, 1)])
+def test_gemm_bf16_residual_in_place(L, cuda, M, N, K, act):
+    """The bf16 residual stream of the bf16 / fp8 modes: out_dtype bf16 with resid aliasing
+    out (resid is read in the output's dtype) on the 256-tile fast epilogues (act 0: pp2b,
+    act > 0: transposed pp2t), their ragged-tile generic epilogue, and the 128-tile kernel."""
+    g = torch.Generator(device=cuda).manual_seed(M + N + K + act)
+    A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
+    Bt = (torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g, device=cuda)
+    x = (4 * torch.randn(M, N, generator=g, device=cuda)).to(torch.bfloat16)
+    x0 = x.double().cpu().numpy()
+    _gemm(L, A, Bt, L.BF16, bias=bias, act=act, resid=x, out=x, out_dtype=1)
+    ref64 = _np_act(act, (A.double() @ Bt.double().T + bias.double()).cpu().numpy()) + x0
+    err = np.abs(x.double().cpu().numpy() - ref64) / np.maximum(np.abs(ref64), 1.0)
+    assert err.max() < 8e-3, err.max()
 
 
 @pytest.mark.parametrize("act", [0, 1])

@@ -65,7 +65,7 @@ def test_quantize_matches_oracle(L, cuda, rows, K, Kq, src):
 @pytest.mark.parametrize("M,N,K,act,out_dtype,resid", [
     (300, 200, 256, 0, 0, False), (1000, 520, 384, 1, 1, False),
     (4096, 1024, 1024, 1, 1, False), (2600, 776, 1536, 0, 0, True),
-    (513, 64, 128, 2, 0, False)])
+    (513, 64, 128, 2, 0, False), (4096, 768, 1536, 1, 1, True), (1000, 520, 384, 0, 1, True)])
 def test_gemm_mx8_matches_dequantized_fp64(L, cuda, M, N, K, act, out_dtype, resid):
     g = torch.Generator(device=cuda).manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
@@ -74,6 +74,8 @@ def test_gemm_mx8_matches_dequantized_fp64(L, cuda, M, N, K, act, out_dtype, res
     qb, sb, sb_rows = _quantize(L, W, K)
     bias = torch.randn(N, generator=g, device=cuda)
     res = torch.randn(M, N, generator=g, device=cuda) if resid else None
+    if resid and out_dtype == 1:
+        res = res.to(torch.bfloat16)                # resid is read in the output's dtype
     out = torch.full((M, N), float("nan"), device=cuda,
                      dtype=torch.float32 if out_dtype == 0 else torch.bfloat16)
     e = L.VtdEpilogue()

@@ -152,7 +152,7 @@ def test_invalid_op_args_raise_before_any_launch(L):
     with pytest.raises(ValueError):
         L.check(L.lib.vtd_attention(None, 1, 4, 1, 48, 144, 1.0, None, 48, L.BF16, None))
     with pytest.raises(ValueError):
-        L.check(L.lib.vtd_layernorm(None, 1, 4, 4, None, None, 1e-3, None, 4, L.F32, None))
+        L.check(L.lib.vtd_layernorm(None, L.F32, 1, 4, 4, None, None, 1e-3, None, 4, L.F32, None))
 
 
 def test_presets_param_counts():

@@ -10,21 +10,34 @@ namespace {
 // ------------------------------------------------------------------ LayerNorm
 // One wave per token row; row held in registers as NV float4 per lane -> exact
 // two-pass mean / biased variance, eps added to the variance (keras default 1e-3).
-template <typename TO, int NV>
+// 4 consecutive elements as f32 (16-B f32 / 8-B bf16 accesses)
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ f32x4 ld4(const bf16_t* p) {
+  const uint2 w = *reinterpret_cast<const uint2*>(p);
+  return f32x4{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+               __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)};
+}
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+__device__ __forceinline__ void st4(bf16_t* p, f32x4 v) {
+  *reinterpret_cast<uint2*>(p) = uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+}
+
+// TI: the residual stream's dtype (f32, or bf16 in the bf16 / fp8 modes); TO: output.
+template <typename TI, typename TO, int NV>
 __global__ __launch_bounds__(256) void layernorm_kernel(
-    const float* __restrict__ x, int64_t rows, int D, int ldx,
+    const TI* __restrict__ x, int64_t rows, int D, int ldx,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
     TO* __restrict__ y, int ldy) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
-  const float* xr = x + row * ldx;
+  const TI* xr = x + row * ldx;
   f32x4 v[NV];
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = (i * 64 + lane) * 4;
-    v[i] = c < D ? *reinterpret_cast<const f32x4*>(xr + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    v[i] = c < D ? ld4(xr + c) : f32x4{0.f, 0.f, 0.f, 0.f};
     s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
   }
 #pragma unroll
@@ -51,63 +64,65 @@ __global__ __launch_bounds__(256) void layernorm_kernel(
     if (c < D) {
       const f32x4 g = *reinterpret_cast<const f32x4*>(gamma + c);
       const f32x4 bb = *reinterpret_cast<const f32x4*>(beta + c);
+      f32x4 o;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) yr[c + j] = DT<TO>::from((v[i][j] - mean) * rstd * g[j] + bb[j]);
+      for (int j = 0; j < 4; ++j) o[j] = (v[i][j] - mean) * rstd * g[j] + bb[j];
+      st4(yr + c, o);
     }
   }
   for (int c = D + lane; c < ldy; c += 64) yr[c] = DT<TO>::from(0.f);
 }
 
-// generic fallback (D % 4 != 0 or D > 4096): three passes over the row
-template <typename TO>
+// generic fallback (unaligned, D % 4 != 0 or D > 4096): three passes over the row
+template <typename TI, typename TO>
 __global__ __launch_bounds__(256) void layernorm_generic_kernel(
-    const float* __restrict__ x, int64_t rows, int D, int ldx,
+    const TI* __restrict__ x, int64_t rows, int D, int ldx,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
     TO* __restrict__ y, int ldy) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
-  const float* xr = x + row * ldx;
+  const TI* xr = x + row * ldx;
   float s = 0.f;
-  for (int c = lane; c < D; c += 64) s += xr[c];
+  for (int c = lane; c < D; c += 64) s += DT<TI>::load(xr + c);
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
   const float mean = s / D;
   float q = 0.f;
   for (int c = lane; c < D; c += 64) {
-    const float d = xr[c] - mean;
+    const float d = DT<TI>::load(xr + c) - mean;
     q += d * d;
   }
   for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
   const float rstd = 1.f / sqrtf(q / D + eps);
   TO* yr = y + row * ldy;
   for (int c = lane; c < ldy; c += 64)
-    yr[c] = DT<TO>::from(c < D ? (xr[c] - mean) * rstd * gamma[c] + beta[c] : 0.f);
+    yr[c] = DT<TO>::from(c < D ? (DT<TI>::load(xr + c) - mean) * rstd * gamma[c] + beta[c] : 0.f);
 }
 
-template <typename TO>
-int ln_dispatch(const float* x, int64_t rows, int D, int ldx, const float* g,
+template <typename TI, typename TO>
+int ln_dispatch(const void* xv, int64_t rows, int D, int ldx, const float* g,
                 const float* b, float eps, void* y, int ldy, hipStream_t st) {
   const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  const TI* x = static_cast<const TI*>(xv);
   TO* yo = static_cast<TO*>(y);
-  const bool vec = (D % 4 == 0) && (ldx % 4 == 0) &&
-                   (reinterpret_cast<uintptr_t>(x) % 16 == 0) &&
+  const bool vec = (D % 4 == 0) && (ldx % 4 == 0) && (ldy % 4 == 0) &&
+                   (reinterpret_cast<uintptr_t>(x) % (4 * sizeof(TI)) == 0) &&
+                   (reinterpret_cast<uintptr_t>(y) % (4 * sizeof(TO)) == 0) &&
                    (reinterpret_cast<uintptr_t>(g) % 16 == 0) &&
                    (reinterpret_cast<uintptr_t>(b) % 16 == 0);
   const int nv = (D + 255) / 256;
-  if (vec && nv <= 1)
-    hipLaunchKernelGGL((layernorm_kernel<TO, 1>), grid, block, 0, st, x, rows, D, ldx, g, b, eps, yo, ldy);
-  else if (vec && nv <= 2)
-    hipLaunchKernelGGL((layernorm_kernel<TO, 2>), grid, block, 0, st, x, rows, D, ldx, g, b, eps, yo, ldy);
-  else if (vec && nv <= 3)
-    hipLaunchKernelGGL((layernorm_kernel<TO, 3>), grid, block, 0, st, x, rows, D, ldx, g, b, eps, yo, ldy);
-  else if (vec && nv <= 4)
-    hipLaunchKernelGGL((layernorm_kernel<TO, 4>), grid, block, 0, st, x, rows, D, ldx, g, b, eps, yo, ldy);
-  else if (vec && nv <= 8)
-    hipLaunchKernelGGL((layernorm_kernel<TO, 8>), grid, block, 0, st, x, rows, D, ldx, g, b, eps, yo, ldy);
-  else if (vec && nv <= 16)
-    hipLaunchKernelGGL((layernorm_kernel<TO, 16>), grid, block, 0, st, x, rows, D, ldx, g, b, eps, yo, ldy);
+#define VTD_LN(NV) hipLaunchKernelGGL((layernorm_kernel<TI, TO, NV>), grid, block, 0, st, x, rows, \
+                                      D, ldx, g, b, eps, yo, ldy)
+  if (vec && nv <= 1) VTD_LN(1);
+  else if (vec && nv <= 2) VTD_LN(2);
+  else if (vec && nv <= 3) VTD_LN(3);
+  else if (vec && nv <= 4) VTD_LN(4);
+  else if (vec && nv <= 8) VTD_LN(8);
+  else if (vec && nv <= 16) VTD_LN(16);
   else
-    hipLaunchKernelGGL((layernorm_generic_kernel<TO>), grid, block, 0, st, x, rows, D, ldx, g, b, eps, yo, ldy);
+    hipLaunchKernelGGL((layernorm_generic_kernel<TI, TO>), grid, block, 0, st, x, rows, D, ldx,
+                       g, b, eps, yo, ldy);
+#undef VTD_LN
   VTD_LAUNCH_CHECK("layernorm");
   return VTD_OK;
 }
@@ -214,15 +229,19 @@ __global__ void pack_vector_kernel(const float* __restrict__ src, int N, int ng,
 
 }  // namespace
 
-int layernorm_launch(const float* x, int64_t rows, int D, int ldx, const float* g,
+int layernorm_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx, const float* g,
                      const float* b, float eps, void* y, int ldy, int dtype,
                      hipStream_t st) {
   VTD_CHECK_ARG(x && g && b && y, "layernorm: null pointer");
   VTD_CHECK_ARG(rows > 0 && D > 0 && ldx >= D && ldy >= D, "layernorm: bad shape");
   VTD_CHECK_ARG(dtype == VTD_F32 || dtype == VTD_BF16, "layernorm: bad dtype");
+  VTD_CHECK_ARG(x_dtype == VTD_F32 || x_dtype == VTD_BF16, "layernorm: bad x dtype");
   ProfScope ps(st, PROF_LN, 0.0);
-  if (dtype == VTD_BF16) return ln_dispatch<bf16_t>(x, rows, D, ldx, g, b, eps, y, ldy, st);
-  return ln_dispatch<float>(x, rows, D, ldx, g, b, eps, y, ldy, st);
+  if (x_dtype == VTD_BF16)
+    return dtype == VTD_BF16 ? ln_dispatch<bf16_t, bf16_t>(x, rows, D, ldx, g, b, eps, y, ldy, st)
+                             : ln_dispatch<bf16_t, float>(x, rows, D, ldx, g, b, eps, y, ldy, st);
+  return dtype == VTD_BF16 ? ln_dispatch<float, bf16_t>(x, rows, D, ldx, g, b, eps, y, ldy, st)
+                           : ln_dispatch<float, float>(x, rows, D, ldx, g, b, eps, y, ldy, st);
 }
 
 int patches_launch(const float* img, int B, int H, int W, int C, int p, void* out,
@@ -262,10 +281,10 @@ int decode_launch(const float* logits, int64_t n, float* dets, hipStream_t st) {
 
 extern "C" {
 
-int vtd_layernorm(const float* x_dev, int64_t rows, int D, int ldx, const float* gamma_dev,
-                  const float* beta_dev, float eps, void* y_dev, int ldy, int dtype,
-                  void* stream) {
-  return vtd::layernorm_launch(x_dev, rows, D, ldx, gamma_dev, beta_dev, eps, y_dev, ldy,
+int vtd_layernorm(const void* x_dev, int x_dtype, int64_t rows, int D, int ldx,
+                  const float* gamma_dev, const float* beta_dev, float eps, void* y_dev, int ldy,
+                  int dtype, void* stream) {
+  return vtd::layernorm_launch(x_dev, x_dtype, rows, D, ldx, gamma_dev, beta_dev, eps, y_dev, ldy,
                                dtype, static_cast<hipStream_t>(stream));
 }
 

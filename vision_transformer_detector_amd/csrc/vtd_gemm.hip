@@ -29,11 +29,33 @@ struct EpiArgs {
   const float* bias;
   const float* rowadd; int rowadd_period; int rowadd_ncols;
   int act;
-  const float* resid; int ldr;
+  const void* resid; int ldr;      // same dtype as out (f32, or the bf16 residual stream)
   void* out; int ldo; int out_dtype;
   void* out2; int ldo2;
   int scatter_tokens;
 };
+
+__device__ __forceinline__ float resid_at(const EpiArgs& e, int64_t i) {
+  return e.out_dtype == VTD_F32 ? static_cast<const float*>(e.resid)[i]
+                                : bf16_to_f32(static_cast<const bf16_t*>(e.resid)[i]);
+}
+__device__ __forceinline__ f32x4 bf16x4_to_f32(uint32_t lo, uint32_t hi) {
+  return f32x4{__uint_as_float(lo << 16), __uint_as_float(lo & 0xffff0000u),
+               __uint_as_float(hi << 16), __uint_as_float(hi & 0xffff0000u)};
+}
+// 8 contiguous residual values (16-B aligned): BF = bf16 residual (one 16-B load)
+template <bool BF>
+__device__ __forceinline__ void load_resid8(const EpiArgs& e, int64_t i, f32x4& r0, f32x4& r1) {
+  if constexpr (BF) {
+    const i32x4 w = *reinterpret_cast<const i32x4*>(static_cast<const bf16_t*>(e.resid) + i);
+    r0 = bf16x4_to_f32((uint32_t)w[0], (uint32_t)w[1]);
+    r1 = bf16x4_to_f32((uint32_t)w[2], (uint32_t)w[3]);
+  } else {
+    const float* p = static_cast<const float*>(e.resid) + i;
+    r0 = *reinterpret_cast<const f32x4*>(p);
+    r1 = *reinterpret_cast<const f32x4*>(p + 4);
+  }
+}
 
 __device__ __forceinline__ int swz(int row, int chunk) {
   return row * KB + ((chunk ^ (row & 7)) << 4);
@@ -45,7 +67,7 @@ __device__ __forceinline__ void epi_store(const EpiArgs& e, int M, int N, int m,
   if (e.bias) v += e.bias[n];
   if (e.rowadd && n < e.rowadd_ncols) v += e.rowadd[m % e.rowadd_period];
   v = apply_act(e.act, v);
-  if (e.resid) v += e.resid[(int64_t)m * e.ldr + n];
+  if (e.resid) v += resid_at(e, (int64_t)m * e.ldr + n);
   int64_t idx;
   if (e.scatter_tokens > 0) {
     // keras Reshape((17, -1)) of a (B, T, 17) tensor (vtd.py:461-463): flat index
@@ -105,7 +127,15 @@ __device__ __forceinline__ void epi_store4(const EpiArgs& e, int M, int N, int m
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) v[j] = apply_act(e.act, v[j]);
-  if (e.resid) v += *reinterpret_cast<const f32x4*>(e.resid + (int64_t)m * e.ldr + n);
+  if (e.resid) {
+    const int64_t ri = (int64_t)m * e.ldr + n;
+    if (e.out_dtype == VTD_F32) {
+      v += *reinterpret_cast<const f32x4*>(static_cast<const float*>(e.resid) + ri);
+    } else {
+      const uint2 w = *reinterpret_cast<const uint2*>(static_cast<const bf16_t*>(e.resid) + ri);
+      v += bf16x4_to_f32(w.x, w.y);
+    }
+  }
   const int64_t idx = (int64_t)m * e.ldo + n;
   if (e.out_dtype == VTD_F32) {
     *reinterpret_cast<f32x4*>(static_cast<float*>(e.out) + idx) = v;
@@ -426,9 +456,7 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
 #pragma unroll
       for (int it = 0; it < NIT; ++it) {
         const int64_t m = m_base + p * PR + it * 8 + rsub;
-        const float* rp = e.resid + m * e.ldr + n_base + c8;
-        rv[it][0] = *reinterpret_cast<const f32x4*>(rp);
-        rv[it][1] = *reinterpret_cast<const f32x4*>(rp + 4);
+        load_resid8<OUT_BF16>(e, m * e.ldr + n_base + c8, rv[it][0], rv[it][1]);
       }
     }
 #pragma unroll
@@ -828,10 +856,8 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int jp = 0; jp < 2; ++jp) {
-          const float* rp = e.resid + (int64_t)(m_base + 16 * (i0 + i) + fr) * e.ldr + n_base +
-                            32 * jp + 8 * fg;
-          rv[i][jp][0] = *reinterpret_cast<const f32x4*>(rp);
-          rv[i][jp][1] = *reinterpret_cast<const f32x4*>(rp + 4);
+          load_resid8<OUT_BF16>(e, (int64_t)(m_base + 16 * (i0 + i) + fr) * e.ldr + n_base +
+                                       32 * jp + 8 * fg, rv[i][jp][0], rv[i][jp][1]);
         }
     }
 #pragma unroll
@@ -975,9 +1001,8 @@ __device__ __forceinline__ void epilogue_fast_x(const f32x4 (&acc)[8][4], float*
     if constexpr (RESID) {
 #pragma unroll
       for (int it = 0; it < 2; ++it) {
-        const float* rp = e.resid + (int64_t)(m_base + p * 16 + it * 8 + rsub) * e.ldr + n_base + c8;
-        rv[it][0] = *reinterpret_cast<const f32x4*>(rp);
-        rv[it][1] = *reinterpret_cast<const f32x4*>(rp + 4);
+        load_resid8<OUT_BF16>(e, (int64_t)(m_base + p * 16 + it * 8 + rsub) * e.ldr + n_base + c8,
+                              rv[it][0], rv[it][1]);
       }
     }
 #pragma unroll

@@ -402,8 +402,9 @@ bool gemm_pp3_launch(int M, int N, int K, const bf16_t* A, int lda, const bf16_t
   if (epi->rowadd || epi->out2 || epi->scatter_tokens > 0) return false;
   if ((int64_t)256 * std::max(lda, ldb) * 2 >= 0x7fffffff) return false;
   if (epi->ldo % 8 != 0 || (epi->resid && epi->ldr % 8 != 0)) return false;
+  if (epi->resid && epi->out_dtype != VTD_F32) return false;   // f32 residual only
   const int tiles_m = (M + BBM - 1) / BBM, tiles_n = (N + BBN - 1) / BBN;
-  const P3Epi e{epi->bias, epi->resid, epi->ldr, epi->out, epi->ldo};
+  const P3Epi e{epi->bias, static_cast<const float*>(epi->resid), epi->ldr, epi->out, epi->ldo};
   const dim3 grid(std::min(tiles_m * tiles_n, num_cu)), block(BNT);
   static bool attr = false;
   if (!attr) {

@@ -15,7 +15,7 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
 int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqkv,
                      float scale, void* out, int ldo, int dtype, hipStream_t stream,
                      double flops);
-int layernorm_launch(const float* x, int64_t rows, int D, int ldx, const float* g,
+int layernorm_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx, const float* g,
                      const float* b, float eps, void* y, int ldy, int dtype, hipStream_t st);
 int patches_launch(const float* img, int B, int H, int W, int C, int p, void* out, int ldo,
                    int dtype, hipStream_t st);
@@ -144,6 +144,16 @@ struct Plan {
 // activation / non-MX matrix dtype of a mode (VTD_FP8 keeps everything else in bf16)
 int act_dtype(int dtype) { return dtype == VTD_FP8 ? VTD_BF16 : dtype; }
 size_t es_of(int dtype) { return act_dtype(dtype) == VTD_BF16 ? 2 : 4; }
+// dtype of the residual stream x: bf16 in the bf16 / fp8 modes (the stream the GEMM
+// epilogues add into and the LayerNorms read), f32 in the f32 mode.  VTD_RESID_F32=1
+// keeps an f32 stream in the bf16 modes (A/B diagnostic; costs ~7 % at C2).
+int resid_dtype(int dtype) {
+  static const bool f32 = [] {
+    const char* v = getenv("VTD_RESID_F32");
+    return v && atoi(v) != 0;
+  }();
+  return act_dtype(dtype) == VTD_BF16 && !f32 ? VTD_BF16 : VTD_F32;
+}
 int k8_of(int k) { return (int)round_up(k, 128); }
 Plan make_plan(const vtd_config* c, const vtd_dims& d) {
   Plan p{};
@@ -224,7 +234,8 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
   VTD_CHECK_ARG(R < (int64_t)1 << 31, "forward: batch*tokens too large");
   const int M = (int)R;
   void* patches = ws + P.patches;
-  float* x = reinterpret_cast<float*>(ws + P.x);
+  const int rdt = resid_dtype(cfg->dtype);
+  void* x = ws + P.x;
   void* xb = ws + P.xb;
   void* h = ws + P.h;
   void* qkv = ws + P.qkv;
@@ -259,7 +270,7 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
     e.bias = w->b_patch;
     e.rowadd = w->pos_embedding; e.rowadd_period = N; e.rowadd_ncols = D;
     e.act = VTD_ACT_NONE;
-    e.out = x; e.ldo = Dp; e.out_dtype = VTD_F32;
+    e.out = x; e.ldo = Dp; e.out_dtype = rdt;
     rc = gemm_launch(M, Dp, d.patch_dim_p, patches, d.patch_dim_p, w->w_patch,
                      d.patch_dim_p, dt, &e, st, 2.0 * fR * D * d.patch_dim);
     if (rc) return rc;
@@ -268,7 +279,7 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
   const float scale = 1.0f / std::sqrt((float)cfg->key_dim);
   for (int i = 0; i < cfg->repeat_times; ++i) {        // vtd.py:350-412
     const vtd_layer_weights& L = w->layers[i];
-    rc = layernorm_launch(x, R, D, Dp, L.ln1_gamma, L.ln1_beta, 1e-3f, h, Dp, dt, st);
+    rc = layernorm_launch(x, rdt, R, D, Dp, L.ln1_gamma, L.ln1_beta, 1e-3f, h, Dp, dt, st);
     if (rc) return rc;
     {
       vtd_epilogue e{};
@@ -286,12 +297,12 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
       vtd_epilogue e{};
       e.bias = L.b_out; e.act = VTD_ACT_NONE;
       e.resid = x; e.ldr = Dp;
-      e.out = x; e.ldo = Dp; e.out_dtype = VTD_F32;
+      e.out = x; e.ldo = Dp; e.out_dtype = rdt;
       rc = enc_gemm(Dp, d.inner_p, attn, L.w_out, L.s_out, &e,
                     2.0 * fR * cfg->num_heads * cfg->key_dim * D);
       if (rc) return rc;
     }
-    rc = layernorm_launch(x, R, D, Dp, L.ln2_gamma, L.ln2_beta, 1e-3f, h, Dp, dt, st);
+    rc = layernorm_launch(x, rdt, R, D, Dp, L.ln2_gamma, L.ln2_beta, 1e-3f, h, Dp, dt, st);
     if (rc) return rc;
     const void* a = h;
     int k = Dp, kv = D;
@@ -301,8 +312,10 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
       e.bias = L.b_mlp[j]; e.act = act;
       if (last) {
         e.resid = x; e.ldr = Dp;
-        e.out = x; e.ldo = Dp; e.out_dtype = VTD_F32;
-        if (i == cfg->repeat_times - 1 && dt == VTD_BF16) { e.out2 = xb; e.ldo2 = Dp; }
+        e.out = x; e.ldo = Dp; e.out_dtype = rdt;
+        if (i == cfg->repeat_times - 1 && dt == VTD_BF16 && rdt == VTD_F32) {
+          e.out2 = xb; e.ldo2 = Dp;           // bf16 copy of an f32 stream for the head
+        }
       } else {
         e.out = mlp[j & 1]; e.ldo = d.mlp_units_p[j]; e.out_dtype = dt;
       }
@@ -322,7 +335,7 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
     e.bias = w->b_det; e.act = VTD_ACT_NONE;
     e.out = u; e.ldo = d.tokens_p; e.out_dtype = dt;
     e.scatter_tokens = N;
-    const void* a = dt == VTD_BF16 ? xb : static_cast<const void*>(x);
+    const void* a = dt == rdt ? x : xb;
     rc = gemm_launch(M, VTD_MAX_DETECT, Dp, a, Dp, w->w_det, Dp, dt, &e, st,
                      2.0 * fR * D * VTD_MAX_DETECT);
     if (rc) return rc;
