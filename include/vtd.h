@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define VTD_ABI_VERSION 3
+#define VTD_ABI_VERSION 4
 #define VTD_KALIGN 64          /* K / row padding granule, elements              */
 #define VTD_MAX_MLP 16         /* max encoder_mlp_quantities                     */
 #define VTD_MAX_HEAD 64        /* max mlp_head layers * repeats                   */
@@ -99,7 +99,12 @@ typedef struct vtd_dims {
  * Vectors: fp32, padded with zeros.
  * VTD_FP8: w_qkv / w_out / w_mlp are MX-fp8 e4m3 [N_p][K8] (K8 = K_p rounded up to 128,
  * vtd_quantize_mx8 of the packed fp32 matrix) and s_* their scales [K8/128][N_p][4];
- * the s_* fields are ignored in the other modes. */
+ * the s_* fields are ignored in the other modes.
+ * LayerNorm fold (VTD_BF16 only): when ln1_colsum is non-NULL, w_qkv / b_qkv hold
+ * vtd_fold_layernorm's W * diag(ln1_gamma) and b + W ln1_beta, ln1_colsum its column
+ * sums, and the forward applies LayerNorm 1 in the query/key/value GEMM's epilogue
+ * (vtd_epilogue.lnstat) instead of a LayerNorm pass; ln2_colsum likewise for LayerNorm 2
+ * and w_mlp[0] / b_mlp[0].  NULL: the LayerNorm kernels run (ln*_gamma / beta used). */
 typedef struct vtd_layer_weights {
   const float* ln1_gamma; const float* ln1_beta;        /* [d_p]                  */
   const void* w_qkv; const float* b_qkv;                /* [qkv_p][d_p], [qkv_p]  */
@@ -108,6 +113,7 @@ typedef struct vtd_layer_weights {
   const void* w_mlp[VTD_MAX_MLP]; const float* b_mlp[VTD_MAX_MLP];
   const uint8_t* s_qkv; const uint8_t* s_out;          /* VTD_FP8 block scales   */
   const uint8_t* s_mlp[VTD_MAX_MLP];
+  const float* ln1_colsum; const float* ln2_colsum;     /* LN fold, or NULL        */
 } vtd_layer_weights;
 
 typedef struct vtd_weights {
@@ -165,6 +171,11 @@ typedef struct vtd_epilogue {
   void* out; int ldo; int out_dtype;
   void* out2; int ldo2;         /* optional bf16 copy                              */
   int scatter_tokens;
+  /* LayerNorm folded into the GEMM (A = the raw rows x, Bt = W * diag(gamma) as stored,
+   * bias = b + W beta): lnstat[2m], lnstat[2m+1] = mean, rstd of row m
+   * (vtd_layernorm_stats) and colsum[n] = sum_k Bt[n][k]; the accumulator becomes
+   * (acc - mean * colsum[n]) * rstd before bias / act.  Both NULL: no fold. */
+  const float* lnstat; const float* colsum;
 } vtd_epilogue;
 int vtd_gemm(int M, int N, int K, const void* A_dev, int lda, const void* Bt_dev,
              int ldb, int dtype, const vtd_epilogue* epi, void* stream);
@@ -190,6 +201,22 @@ int vtd_gemm_mx8(int M, int N, int K, const uint8_t* A_dev, int lda, const uint8
 int vtd_layernorm(const void* x_dev, int x_dtype, int64_t rows, int D, int ldx,
                   const float* gamma_dev, const float* beta_dev, float eps,
                   void* y_dev, int ldy, int dtype, void* stream);
+
+/* Row statistics of keras LayerNormalization (the same two-pass fp32 mean / biased
+ * variance as vtd_layernorm): stat[2r] = mean, stat[2r+1] = 1 / sqrt(var + eps) of the
+ * first D columns of row r of x (x_dtype F32 or BF16). */
+int vtd_layernorm_stats(const void* x_dev, int x_dtype, int64_t rows, int D, int ldx,
+                        float eps, float* stat_dev, void* stream);
+
+/* Folds LayerNorm(gamma, beta) into the Dense layer that consumes it: w32 fp32 packed
+ * W^T [N][ldw] (first K columns used) -> w_out (dtype) [N][ldo] = W^T[n][k] * gamma[k]
+ * (columns [K, ldo) zero), bias_out[n] = bias_in[n] + sum_k W^T[n][k] beta[k] and
+ * colsum[n] = sum_k w_out[n][k] (of the stored, rounded values); fp64 sums.
+ * LN(x) W + b == (x W' - mean * colsum) * rstd + bias_out, exactly in real arithmetic. */
+int vtd_fold_layernorm(const float* w32_dev, int N, int K, int ldw, const float* gamma_dev,
+                       const float* beta_dev, const float* bias_in_dev, void* w_out_dev,
+                       int ldo, int dtype, float* bias_out_dev, float* colsum_dev,
+                       void* stream);
 
 /* keras MultiHeadAttention core (vtd.py:364-369): per batch b, head h,
  * O = softmax(scale * Q K^T) V with Q, K, V read from qkv [B*N][ldqkv] at column

@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede loading libvtd.so, see module doc)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvtd.so")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 KALIGN = 64
 MAX_MLP = 16
 MAX_HEAD = 64
@@ -55,7 +55,8 @@ class VtdLayerWeights(ctypes.Structure):
         ("b_qkv", c_void_p), ("w_out", c_void_p), ("b_out", c_void_p),
         ("ln2_gamma", c_void_p), ("ln2_beta", c_void_p),
         ("w_mlp", c_void_p * MAX_MLP), ("b_mlp", c_void_p * MAX_MLP),
-        ("s_qkv", c_void_p), ("s_out", c_void_p), ("s_mlp", c_void_p * MAX_MLP)]
+        ("s_qkv", c_void_p), ("s_out", c_void_p), ("s_mlp", c_void_p * MAX_MLP),
+        ("ln1_colsum", c_void_p), ("ln2_colsum", c_void_p)]
 
 
 class VtdWeights(ctypes.Structure):
@@ -71,7 +72,7 @@ class VtdEpilogue(ctypes.Structure):
         ("bias", c_void_p), ("rowadd", c_void_p), ("rowadd_period", c_int),
         ("rowadd_ncols", c_int), ("act", c_int), ("resid", c_void_p), ("ldr", c_int),
         ("out", c_void_p), ("ldo", c_int), ("out_dtype", c_int), ("out2", c_void_p),
-        ("ldo2", c_int), ("scatter_tokens", c_int)]
+        ("ldo2", c_int), ("scatter_tokens", c_int), ("lnstat", c_void_p), ("colsum", c_void_p)]
 
 
 # name -> (restype, argtypes)
@@ -93,6 +94,10 @@ SIGNATURES = {
                              c_int, c_void_p, c_int64, ctypes.POINTER(VtdEpilogue), c_void_p]),
     "vtd_layernorm": (c_int, [c_void_p, c_int, c_int64, c_int, c_int, c_void_p, c_void_p, c_float,
                               c_void_p, c_int, c_int, c_void_p]),
+    "vtd_layernorm_stats": (c_int, [c_void_p, c_int, c_int64, c_int, c_int, c_float, c_void_p,
+                                    c_void_p]),
+    "vtd_fold_layernorm": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "vtd_attention": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_float,
                               c_void_p, c_int, c_int, c_void_p]),
     "vtd_decode": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),

@@ -127,6 +127,147 @@ int ln_dispatch(const void* xv, int64_t rows, int D, int ldx, const float* g,
   return VTD_OK;
 }
 
+// LayerNorm row statistics only (the fold path, vtd_epilogue.lnstat): one wave per RPW
+// rows (all their loads issued before the first reduction: the pass is a pure read
+// stream and needs the loads in flight), the same two-pass mean / variance as
+// layernorm_kernel; stat[r] = (mean, rstd).
+constexpr int LS_RPW = 2;
+// 8 consecutive elements as two f32x4 (one 16-B bf16 load / two 16-B f32 loads)
+__device__ __forceinline__ void ld8(const float* p, f32x4& a, f32x4& b) {
+  a = *reinterpret_cast<const f32x4*>(p);
+  b = *reinterpret_cast<const f32x4*>(p + 4);
+}
+__device__ __forceinline__ void ld8(const bf16_t* p, f32x4& a, f32x4& b) {
+  const uint4 w = *reinterpret_cast<const uint4*>(p);
+  a = f32x4{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+            __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)};
+  b = f32x4{__uint_as_float(w.z << 16), __uint_as_float(w.z & 0xffff0000u),
+            __uint_as_float(w.w << 16), __uint_as_float(w.w & 0xffff0000u)};
+}
+template <typename TI, int NV>      // NV = 8-element chunks per lane (D <= 512 NV)
+__global__ __launch_bounds__(256) void ln_stats_kernel(const TI* __restrict__ x, int64_t rows,
+                                                       int D, int ldx, float eps,
+                                                       float2* __restrict__ stat) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * LS_RPW;
+  if (row0 >= rows) return;
+  f32x4 v[LS_RPW][NV][2];
+#pragma unroll
+  for (int r = 0; r < LS_RPW; ++r) {
+    const TI* xr = x + min(row0 + r, rows - 1) * ldx;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (i * 64 + lane) * 8;
+      if (c < D) {
+        ld8(xr + c, v[r][i][0], v[r][i][1]);
+      } else {
+        v[r][i][0] = v[r][i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < LS_RPW; ++r) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) s += v[r][i][h][0] + v[r][i][h][1] + v[r][i][h][2] + v[r][i][h][3];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    const float mean = s / D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (i * 64 + lane) * 8;
+      if (c < D)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float d = v[r][i][h][j] - mean;
+            q += d * d;
+          }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+    if (lane == 0 && row0 + r < rows) stat[row0 + r] = float2{mean, 1.f / sqrtf(q / D + eps)};
+  }
+}
+
+template <typename TI>
+__global__ __launch_bounds__(256) void ln_stats_generic_kernel(const TI* __restrict__ x,
+                                                               int64_t rows, int D, int ldx,
+                                                               float eps, float2* __restrict__ stat) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const TI* xr = x + row * ldx;
+  float s = 0.f;
+  for (int c = lane; c < D; c += 64) s += DT<TI>::load(xr + c);
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const float mean = s / D;
+  float q = 0.f;
+  for (int c = lane; c < D; c += 64) {
+    const float d = DT<TI>::load(xr + c) - mean;
+    q += d * d;
+  }
+  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+  if (lane == 0) stat[row] = float2{mean, 1.f / sqrtf(q / D + eps)};
+}
+
+template <typename TI>
+void ln_stats_dispatch(const void* xv, int64_t rows, int D, int ldx, float eps, float2* stat,
+                       hipStream_t st) {
+  const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  const TI* x = static_cast<const TI*>(xv);
+  const bool vec = (D % 8 == 0) && (ldx % 8 == 0) &&
+                   (reinterpret_cast<uintptr_t>(x) % 16 == 0);
+  const int nv = (D + 511) / 512;
+  const dim3 gridv((unsigned)((rows + 4 * LS_RPW - 1) / (4 * LS_RPW)));
+#define VTD_LS(NV) hipLaunchKernelGGL((ln_stats_kernel<TI, NV>), gridv, block, 0, st, x, rows, D, \
+                                      ldx, eps, stat)
+  if (vec && nv <= 1) VTD_LS(1);
+  else if (vec && nv <= 2) VTD_LS(2);
+  else if (vec && nv <= 4) VTD_LS(4);
+  else
+    hipLaunchKernelGGL((ln_stats_generic_kernel<TI>), grid, block, 0, st, x, rows, D, ldx, eps,
+                       stat);
+#undef VTD_LS
+}
+
+// LayerNorm fold of one consumer Dense layer (one-time weight preparation): one wave per
+// output row n; fp64 sums (bias' from the fp32 W, colsum from the rounded stored W').
+template <typename TO>
+__global__ __launch_bounds__(256) void fold_ln_kernel(const float* __restrict__ w, int N, int K,
+                                                      int ldw, const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta,
+                                                      const float* __restrict__ bias_in,
+                                                      TO* __restrict__ wo, int ldo,
+                                                      float* __restrict__ bias_out,
+                                                      float* __restrict__ colsum) {
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= N) return;
+  double sb = 0.0, sc = 0.0;
+  for (int k = lane; k < ldo; k += 64) {
+    const float wk = k < K ? w[(int64_t)n * ldw + k] : 0.f;
+    const TO q = DT<TO>::from(k < K ? wk * gamma[k] : 0.f);
+    wo[(int64_t)n * ldo + k] = q;
+    if (k < K) {
+      sb += (double)wk * (double)beta[k];
+      sc += (double)DT<TO>::load(&q);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    sb += __shfl_xor(sb, o);
+    sc += __shfl_xor(sc, o);
+  }
+  if (lane == 0) {
+    bias_out[n] = (float)((double)(bias_in ? bias_in[n] : 0.f) + sb);
+    colsum[n] = (float)sc;
+  }
+}
+
 // ------------------------------------------------------------------ patches
 // tf.image.extract_patches(SAME, size = stride = p) + Reshape: output row m = b*N + t
 // (t = gy*gw + gx), column k = (kh*p + kw)*C + c; outside the image -> 0.
@@ -244,6 +385,37 @@ int layernorm_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx, c
                            : ln_dispatch<float, float>(x, rows, D, ldx, g, b, eps, y, ldy, st);
 }
 
+int ln_stats_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx, float eps,
+                    float* stat, hipStream_t st) {
+  VTD_CHECK_ARG(x && stat, "layernorm_stats: null pointer");
+  VTD_CHECK_ARG(rows > 0 && D > 0 && ldx >= D, "layernorm_stats: bad shape");
+  VTD_CHECK_ARG(x_dtype == VTD_F32 || x_dtype == VTD_BF16, "layernorm_stats: bad x dtype");
+  VTD_CHECK_ARG(reinterpret_cast<uintptr_t>(stat) % 8 == 0, "layernorm_stats: stat alignment");
+  ProfScope ps(st, PROF_LN, 0.0);
+  float2* s2 = reinterpret_cast<float2*>(stat);
+  if (x_dtype == VTD_BF16) ln_stats_dispatch<bf16_t>(x, rows, D, ldx, eps, s2, st);
+  else ln_stats_dispatch<float>(x, rows, D, ldx, eps, s2, st);
+  VTD_LAUNCH_CHECK("layernorm_stats");
+  return VTD_OK;
+}
+
+int fold_ln_launch(const float* w, int N, int K, int ldw, const float* gamma, const float* beta,
+                   const float* bias_in, void* wo, int ldo, int dtype, float* bias_out,
+                   float* colsum, hipStream_t st) {
+  VTD_CHECK_ARG(w && gamma && beta && wo && bias_out && colsum, "fold_layernorm: null pointer");
+  VTD_CHECK_ARG(N > 0 && K > 0 && ldw >= K && ldo >= K, "fold_layernorm: bad shape");
+  VTD_CHECK_ARG(dtype == VTD_F32 || dtype == VTD_BF16, "fold_layernorm: bad dtype");
+  const dim3 grid((unsigned)((N + 3) / 4)), block(256);
+  if (dtype == VTD_BF16)
+    hipLaunchKernelGGL(fold_ln_kernel<bf16_t>, grid, block, 0, st, w, N, K, ldw, gamma, beta,
+                       bias_in, static_cast<bf16_t*>(wo), ldo, bias_out, colsum);
+  else
+    hipLaunchKernelGGL(fold_ln_kernel<float>, grid, block, 0, st, w, N, K, ldw, gamma, beta,
+                       bias_in, static_cast<float*>(wo), ldo, bias_out, colsum);
+  VTD_LAUNCH_CHECK("fold_layernorm");
+  return VTD_OK;
+}
+
 int patches_launch(const float* img, int B, int H, int W, int C, int p, void* out,
                    int ldo, int dtype, hipStream_t st) {
   VTD_CHECK_ARG(img && out, "extract_patches: null pointer");
@@ -286,6 +458,21 @@ int vtd_layernorm(const void* x_dev, int x_dtype, int64_t rows, int D, int ldx,
                   int dtype, void* stream) {
   return vtd::layernorm_launch(x_dev, x_dtype, rows, D, ldx, gamma_dev, beta_dev, eps, y_dev, ldy,
                                dtype, static_cast<hipStream_t>(stream));
+}
+
+int vtd_layernorm_stats(const void* x_dev, int x_dtype, int64_t rows, int D, int ldx,
+                        float eps, float* stat_dev, void* stream) {
+  return vtd::ln_stats_launch(x_dev, x_dtype, rows, D, ldx, eps, stat_dev,
+                              static_cast<hipStream_t>(stream));
+}
+
+int vtd_fold_layernorm(const float* w32_dev, int N, int K, int ldw, const float* gamma_dev,
+                       const float* beta_dev, const float* bias_in_dev, void* w_out_dev,
+                       int ldo, int dtype, float* bias_out_dev, float* colsum_dev,
+                       void* stream) {
+  return vtd::fold_ln_launch(w32_dev, N, K, ldw, gamma_dev, beta_dev, bias_in_dev, w_out_dev,
+                             ldo, dtype, bias_out_dev, colsum_dev,
+                             static_cast<hipStream_t>(stream));
 }
 
 int vtd_extract_patches(const float* images_dev, int B, int H, int W, int C, int p,

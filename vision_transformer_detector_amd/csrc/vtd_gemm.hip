@@ -33,6 +33,9 @@ struct EpiArgs {
   void* out; int ldo; int out_dtype;
   void* out2; int ldo2;
   int scatter_tokens;
+  // LayerNorm folded into this GEMM (A = the raw residual stream): per row (mean, rstd),
+  // per column colsum[n] = sum_k Bt[n][k]; acc -> (acc - mean * colsum) * rstd first
+  const float2* lnstat; const float* colsum;
 };
 
 __device__ __forceinline__ float resid_at(const EpiArgs& e, int64_t i) {
@@ -64,6 +67,10 @@ __device__ __forceinline__ int swz(int row, int chunk) {
 __device__ __forceinline__ void epi_store(const EpiArgs& e, int M, int N, int m, int n,
                                           float v) {
   if (m >= M || n >= N) return;
+  if (e.lnstat) {
+    const float2 st = e.lnstat[m];
+    v = (v - st.x * e.colsum[n]) * st.y;
+  }
   if (e.bias) v += e.bias[n];
   if (e.rowadd && n < e.rowadd_ncols) v += e.rowadd[m % e.rowadd_period];
   v = apply_act(e.act, v);
@@ -115,6 +122,10 @@ __device__ __forceinline__ void epi_store4(const EpiArgs& e, int M, int N, int m
 #pragma unroll
     for (int j = 0; j < 4; ++j) epi_store(e, M, N, m, n + j, v[j]);
     return;
+  }
+  if (e.lnstat) {
+    const float2 st = e.lnstat[m];
+    v = (v - st.x * *reinterpret_cast<const f32x4*>(e.colsum + n)) * st.y;
   }
   if (e.bias) {
     const f32x4 b = *reinterpret_cast<const f32x4*>(e.bias + n);
@@ -425,12 +436,30 @@ __device__ __forceinline__ void epi_out2_8(const EpiArgs& e, int m, int n, f32x4
   *reinterpret_cast<i32x4*>(static_cast<bf16_t*>(e.out2) + (int64_t)m * e.ldo2 + n) = o;
 }
 
+// LayerNorm fold of 8 contiguous columns of row m (c0, c1 = colsum of those columns).
+// lst (the pp2 kernels): the (mean, rstd) of the wave's 128 rows, loaded before the K
+// loop, lane l holding local rows l (lst[0]) and 64 + l (lst[1]); lr = m's local row.
+__device__ __forceinline__ void epi_lnfold8(const EpiArgs& e, const float2* lst, int m, int lr,
+                                            f32x4 c0, f32x4 c1, f32x4& v0, f32x4& v1) {
+  float2 st;
+  if (lst) {
+    const float2 h = (lr & 64) ? lst[1] : lst[0];
+    st.x = __shfl(h.x, lr & 63);
+    st.y = __shfl(h.y, lr & 63);
+  } else {
+    st = e.lnstat[m];
+  }
+  v0 = (v0 - st.x * c0) * st.y;
+  v1 = (v1 - st.x * c1) * st.y;
+}
+
 // Writes the wave's 128 x 64 accumulator tile: 4 passes of 32 rows staged through the
 // wave's private LDS region; each lane then owns 8 consecutive columns of a row, so
 // residual reads and output writes are 16-B per lane (one 128-B line per 8 lanes).
 template <int EPI, bool kDiagNoStore = false, int PR = 32>
 __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* ep, int lane,
-                                              int m_base, int n_base, const EpiArgs& e) {
+                                              int m_base, int n_base, const EpiArgs& e,
+                                              const float2* lst = nullptr) {
   constexpr int ACT = EPI & 3;
   constexpr bool OUT_BF16 = (EPI & 4) != 0;
   constexpr bool RESID = (EPI & 8) != 0;
@@ -441,6 +470,11 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
   const int c8 = (lane & 7) * 8, rsub = lane >> 3;
   const f32x4 b0 = *reinterpret_cast<const f32x4*>(e.bias + n_base + c8);
   const f32x4 b1 = *reinterpret_cast<const f32x4*>(e.bias + n_base + c8 + 4);
+  f32x4 cs0 = {}, cs1 = {};
+  if (e.lnstat) {
+    cs0 = *reinterpret_cast<const f32x4*>(e.colsum + n_base + c8);
+    cs1 = *reinterpret_cast<const f32x4*>(e.colsum + n_base + c8 + 4);
+  }
   if (e.scatter_tokens == -2) m_base &= 255;   // timing diagnostic (VTD_GEMM_VARIANT=5)
 #pragma unroll
   for (int p = 0; p < 128 / PR; ++p) {
@@ -462,8 +496,11 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
       const int row = it * 8 + rsub;
-      f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + row * ES + c8) + b0;
-      f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + row * ES + c8 + 4) + b1;
+      f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + row * ES + c8);
+      f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + row * ES + c8 + 4);
+      if (e.lnstat) epi_lnfold8(e, lst, m_base + p * PR + row, p * PR + row, cs0, cs1, v0, v1);
+      v0 += b0;
+      v1 += b1;
       if (e.rowadd) epi_rowadd8(e, m_base + p * PR + row, n_base + c8, v0, v1);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -837,17 +874,21 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
 // = last 4).  Bias is loaded once; residual rows are fetched 4 row blocks at a time.
 template <int EPI>
 __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int lane, int m_base,
-                                                int n_base, const EpiArgs& e) {
+                                                int n_base, const EpiArgs& e,
+                                                const float2* lst = nullptr) {
   constexpr int ACT = EPI & 3;
   constexpr bool OUT_BF16 = (EPI & 4) != 0;
   constexpr bool RESID = (EPI & 8) != 0;
   const int fr = lane & 15, fg = lane >> 4;
-  f32x4 bias[2][2];
+  f32x4 bias[2][2], cs[2][2] = {};
 #pragma unroll
   for (int jp = 0; jp < 2; ++jp)
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < 2; ++h) {
       bias[jp][h] = *reinterpret_cast<const f32x4*>(e.bias + n_base + 32 * jp + 8 * fg + 4 * h);
+      if (e.lnstat)
+        cs[jp][h] = *reinterpret_cast<const f32x4*>(e.colsum + n_base + 32 * jp + 8 * fg + 4 * h);
+    }
 #pragma unroll
   for (int i0 = 0; i0 < 8; i0 += 4) {
     f32x4 rv[4][2][2];
@@ -864,9 +905,13 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int jp = 0; jp < 2; ++jp) {
-        f32x4 v0 = acc[i0 + i][2 * jp] + bias[jp][0];
-        f32x4 v1 = acc[i0 + i][2 * jp + 1] + bias[jp][1];
+        f32x4 v0 = acc[i0 + i][2 * jp];
+        f32x4 v1 = acc[i0 + i][2 * jp + 1];
         const int mrow = m_base + 16 * (i0 + i) + fr, ncol = n_base + 32 * jp + 8 * fg;
+        if (e.lnstat)
+          epi_lnfold8(e, lst, mrow, 16 * (i0 + i) + fr, cs[jp][0], cs[jp][1], v0, v1);
+        v0 += bias[jp][0];
+        v1 += bias[jp][1];
         if (e.rowadd) epi_rowadd8(e, mrow, ncol, v0, v1);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -935,6 +980,13 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
     pp2b_sources<TR>(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane);
   else
     pp2_sources(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane);
+  // LayerNorm-fold row statistics of the wave's 128 rows: issued before the K loop (the
+  // oldest vector-memory op, so the loop's counted waits retire it), used in the epilogue
+  float2 lst[2] = {float2{0.f, 0.f}, float2{0.f, 0.f}};
+  if (e.lnstat) {
+    lst[0] = e.lnstat[min(m0 + wm * 128 + lane, M - 1)];
+    lst[1] = e.lnstat[min(m0 + wm * 128 + 64 + lane, M - 1)];
+  }
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -946,7 +998,7 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
   if constexpr (TR) {
     if constexpr (EPI != EPI_GENERIC) {
       if (m0 + BBM <= M && n0 + BBN <= N) {
-        epilogue_direct<EPI>(acc, lane, m_base, n_base, e);
+        epilogue_direct<EPI>(acc, lane, m_base, n_base, e, lst);
         return;
       }
     }
@@ -957,7 +1009,7 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
   float* ep = reinterpret_cast<float*>(smem) + wave * 32 * 68;
   if constexpr (EPI != EPI_GENERIC) {
     if (m0 + BBM <= M && n0 + BBN <= N) {
-      epilogue_fast<EPI>(acc, ep, lane, m_base, n_base, e);
+      epilogue_fast<EPI>(acc, ep, lane, m_base, n_base, e, lst);
       return;
     }
   }
@@ -1535,10 +1587,13 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
   VTD_CHECK_ARG(!epi->rowadd || epi->rowadd_period > 0, "gemm: rowadd_period");
   VTD_CHECK_ARG(epi->scatter_tokens <= 0 || N <= VTD_MAX_DETECT,
                 "gemm: scatter epilogue needs N <= 17");
+  VTD_CHECK_ARG(!epi->lnstat || (epi->colsum && reinterpret_cast<uintptr_t>(epi->lnstat) % 8 == 0 &&
+                                 reinterpret_cast<uintptr_t>(epi->colsum) % 16 == 0),
+                "gemm: lnstat needs colsum (16-B aligned) and 8-B alignment");
   EpiArgs e{epi->bias, epi->rowadd, epi->rowadd_period,
             epi->rowadd ? epi->rowadd_ncols : 0, epi->act, epi->resid, epi->ldr,
             epi->out, epi->ldo, epi->out_dtype, epi->out2, epi->ldo2,
-            epi->scatter_tokens};
+            epi->scatter_tokens, reinterpret_cast<const float2*>(epi->lnstat), epi->colsum};
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM);
   const size_t lds = 4 * TILE_BYTES;
   ProfScope ps(stream, PROF_GEMM, flops > 0 ? flops : 2.0 * M * N * (double)K);
@@ -1598,7 +1653,7 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
       // pp2p (7) and pp3 (11), whose epilogues do not implement them
       const bool rare_ok = variant != 7 && variant != 11 &&
                            (!e.out2 || (e.ldo2 % 8 == 0 && reinterpret_cast<uintptr_t>(e.out2) % 16 == 0));
-      const bool fast = e.bias && (rare_ok || (!e.rowadd && !e.out2)) &&
+      const bool fast = e.bias && (rare_ok || (!e.rowadd && !e.out2 && !e.lnstat)) &&
                         (e.scatter_tokens <= 0 || variant == 5) &&
                         e.ldo % 8 == 0 && (!e.resid || e.ldr % 8 == 0) &&
                         reinterpret_cast<uintptr_t>(e.out) % 16 == 0 &&
@@ -1709,10 +1764,13 @@ int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_
   VTD_CHECK_ARG(!epi->rowadd || epi->rowadd_period > 0, "gemm_mx8: rowadd_period");
   VTD_CHECK_ARG(epi->scatter_tokens <= 0 || N <= VTD_MAX_DETECT,
                 "gemm_mx8: scatter epilogue needs N <= 17");
+  VTD_CHECK_ARG(!epi->lnstat || (epi->colsum && reinterpret_cast<uintptr_t>(epi->lnstat) % 8 == 0 &&
+                                 reinterpret_cast<uintptr_t>(epi->colsum) % 16 == 0),
+                "gemm_mx8: lnstat needs colsum (16-B aligned) and 8-B alignment");
   EpiArgs e{epi->bias, epi->rowadd, epi->rowadd_period,
             epi->rowadd ? epi->rowadd_ncols : 0, epi->act, epi->resid, epi->ldr,
             epi->out, epi->ldo, epi->out_dtype, epi->out2, epi->ldo2,
-            epi->scatter_tokens};
+            epi->scatter_tokens, reinterpret_cast<const float2*>(epi->lnstat), epi->colsum};
   ProfScope ps(stream, PROF_GEMM, flops > 0 ? flops : 2.0 * M * N * (double)K);
   const int tiles_m = (M + BBM - 1) / BBM, tiles_n = (N + BBN - 1) / BBN;
   static bool attr = false;

@@ -17,6 +17,8 @@ int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqk
                      double flops);
 int layernorm_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx, const float* g,
                      const float* b, float eps, void* y, int ldy, int dtype, hipStream_t st);
+int ln_stats_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx, float eps,
+                    float* stat, hipStream_t st);
 int patches_launch(const float* img, int B, int H, int W, int C, int p, void* out, int ldo,
                    int dtype, hipStream_t st);
 int decode_launch(const float* logits, int64_t n, float* dets, hipStream_t st);
@@ -137,7 +139,7 @@ static int derive(const vtd_config* c, vtd_dims* d) {
 
 namespace {
 struct Plan {
-  size_t patches, x, xb, h, qkv, attn, mlp0, mlp1, u, head0, head1, q8, s8, total;
+  size_t patches, x, xb, h, stat, qkv, attn, mlp0, mlp1, u, head0, head1, q8, s8, total;
   int k8_max;                       // widest MX-fp8 GEMM K (VTD_FP8)
   int64_t s8_rows;                  // activation scale rows (rows rounded up to 4)
 };
@@ -172,6 +174,7 @@ Plan make_plan(const vtd_config* c, const vtd_dims& d) {
   p.x = take(R * d.d_p * 4);
   p.xb = take(act_dtype(c->dtype) == VTD_BF16 ? R * d.d_p * 2 : 0);
   p.h = take(R * d.d_p * es);
+  p.stat = take(R * 8);                 // LayerNorm (mean, rstd) per row, fold path
   p.qkv = take(R * d.qkv_p * es);
   p.attn = take(R * d.inner_p * es);
   p.mlp0 = take(R * mlp_max * es);
@@ -235,6 +238,7 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
   const int M = (int)R;
   void* patches = ws + P.patches;
   const int rdt = resid_dtype(cfg->dtype);
+  float* stat = reinterpret_cast<float*>(ws + P.stat);
   void* x = ws + P.x;
   void* xb = ws + P.xb;
   void* h = ws + P.h;
@@ -279,13 +283,23 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
   const float scale = 1.0f / std::sqrt((float)cfg->key_dim);
   for (int i = 0; i < cfg->repeat_times; ++i) {        // vtd.py:350-412
     const vtd_layer_weights& L = w->layers[i];
-    rc = layernorm_launch(x, rdt, R, D, Dp, L.ln1_gamma, L.ln1_beta, 1e-3f, h, Dp, dt, st);
+    if (fp8 && (L.ln1_colsum || L.ln2_colsum))
+      return fail(VTD_ERR_UNSUPPORTED, "forward: LayerNorm fold (ln*_colsum) is not supported in VTD_FP8 mode");
+    // LayerNorm 1: its own pass into h, or folded into the query/key/value GEMM
+    const void* a1 = h;
+    if (L.ln1_colsum) {
+      rc = ln_stats_launch(x, rdt, R, D, Dp, 1e-3f, stat, st);
+      a1 = x;
+    } else {
+      rc = layernorm_launch(x, rdt, R, D, Dp, L.ln1_gamma, L.ln1_beta, 1e-3f, h, Dp, dt, st);
+    }
     if (rc) return rc;
     {
       vtd_epilogue e{};
       e.bias = L.b_qkv; e.act = VTD_ACT_NONE;
       e.out = qkv; e.ldo = d.qkv_p; e.out_dtype = dt;
-      rc = enc_gemm(d.qkv_p, Dp, h, L.w_qkv, L.s_qkv, &e,
+      if (L.ln1_colsum) { e.lnstat = stat; e.colsum = L.ln1_colsum; }
+      rc = enc_gemm(d.qkv_p, Dp, a1, L.w_qkv, L.s_qkv, &e,
                     2.0 * fR * D * 3.0 * cfg->num_heads * cfg->key_dim);
       if (rc) return rc;
     }
@@ -302,14 +316,20 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
                     2.0 * fR * cfg->num_heads * cfg->key_dim * D);
       if (rc) return rc;
     }
-    rc = layernorm_launch(x, rdt, R, D, Dp, L.ln2_gamma, L.ln2_beta, 1e-3f, h, Dp, dt, st);
-    if (rc) return rc;
     const void* a = h;
+    if (L.ln2_colsum) {
+      rc = ln_stats_launch(x, rdt, R, D, Dp, 1e-3f, stat, st);
+      a = x;
+    } else {
+      rc = layernorm_launch(x, rdt, R, D, Dp, L.ln2_gamma, L.ln2_beta, 1e-3f, h, Dp, dt, st);
+    }
+    if (rc) return rc;
     int k = Dp, kv = D;
     for (int j = 0; j < q; ++j) {
       const bool last = j == q - 1;
       vtd_epilogue e{};
       e.bias = L.b_mlp[j]; e.act = act;
+      if (j == 0 && L.ln2_colsum) { e.lnstat = stat; e.colsum = L.ln2_colsum; }
       if (last) {
         e.resid = x; e.ldr = Dp;
         e.out = x; e.ldo = Dp; e.out_dtype = rdt;

@@ -15,6 +15,7 @@ fp32 pre-sigmoid logits out.
 from __future__ import annotations
 
 import ctypes
+import os
 import math
 from collections import OrderedDict
 from enum import Enum
@@ -282,6 +283,23 @@ class Model:
             return mx8(dense(name, rows_p, k_p, dst=f32_staging(rows_p, k_p), pdt=L.F32, **kw),
                        name)
 
+        # LayerNorm fold (bf16 mode): LN1 into query/key/value, LN2 into the first MLP
+        # layer (vtd_fold_layernorm); the forward then runs vtd_layernorm_stats instead of
+        # the LayerNorm passes.  VTD_LN_FOLD=0 keeps the LayerNorm passes (A/B switch).
+        fold = self.dtype == L.BF16 and os.environ.get("VTD_LN_FOLD", "1") != "0"
+
+        def fold_ln(w32, b32, gamma, beta):
+            """(W * diag(gamma), b + W beta, colsum) of a packed fp32 [N_p][K_p] matrix."""
+            n_p, k_p = w32.shape
+            wo = zeros(n_p, k_p)
+            bo = zeros(n_p, dtype=torch.float32)
+            cs = zeros(n_p, dtype=torch.float32)
+            L.check(L.lib.vtd_fold_layernorm(w32.data_ptr(), n_p, k_p, k_p, gamma.data_ptr(),
+                                             beta.data_ptr(), b32.data_ptr(), wo.data_ptr(),
+                                             k_p, dt, bo.data_ptr(), cs.data_ptr(), stream),
+                    "fold_layernorm")
+            return wo.data_ptr(), bo.data_ptr(), cs.data_ptr()
+
         def vector(name, n_p, ng=None, ngp=None, dst=None, off=0):
             v = src(name).reshape(-1)
             if dst is None:
@@ -306,20 +324,23 @@ class Model:
             ln2 = f"layer_normalization_{2 * i - 1}"
             mha = "multi_head_attention" if i == 1 else f"multi_head_attention_{i - 1}"
             Ly = layers[i - 1]
-            Ly.ln1_gamma = vector(f"{ln1}/gamma", dims.d_p).data_ptr()
-            Ly.ln1_beta = vector(f"{ln1}/beta", dims.d_p).data_ptr()
-            Ly.ln2_gamma = vector(f"{ln2}/gamma", dims.d_p).data_ptr()
-            Ly.ln2_beta = vector(f"{ln2}/beta", dims.d_p).data_ptr()
-            wqkv = f32_staging(dims.qkv_p, dims.d_p) if fp8 else zeros(dims.qkv_p, dims.d_p)
+            g1, b1 = vector(f"{ln1}/gamma", dims.d_p), vector(f"{ln1}/beta", dims.d_p)
+            g2, b2 = vector(f"{ln2}/gamma", dims.d_p), vector(f"{ln2}/beta", dims.d_p)
+            Ly.ln1_gamma, Ly.ln1_beta = g1.data_ptr(), b1.data_ptr()
+            Ly.ln2_gamma, Ly.ln2_beta = g2.data_ptr(), b2.data_ptr()
+            wqkv = (f32_staging(dims.qkv_p, dims.d_p) if fp8 or fold
+                    else zeros(dims.qkv_p, dims.d_p))
             bqkv = zeros(dims.qkv_p, dtype=torch.float32)
             for part_i, part in enumerate(("query", "key", "value")):
                 off = part_i * dims.inner_p
                 # EinsumDense kernel (D, H, dk) -> (D, H*dk); columns padded per head
                 dense(f"{mha}/{part}", None, dims.d_p, ng=dk, ngp=dkp, dst=wqkv, off=off,
-                      pdt=L.F32 if fp8 else None)
+                      pdt=L.F32 if fp8 or fold else None)
                 vector(f"{mha}/{part}/bias", None, ng=dk, ngp=dkp, dst=bqkv, off=off)
             Ly.w_qkv, Ly.s_qkv = mx8(wqkv, f"{mha}/qkv") if fp8 else (wqkv.data_ptr(), None)
             Ly.b_qkv = bqkv.data_ptr()
+            if fold:
+                Ly.w_qkv, Ly.b_qkv, Ly.ln1_colsum = fold_ln(wqkv, bqkv, g1, b1)
             # attention_output kernel (H, dk, D) -> (H*dk, D); rows padded per head
             Ly.w_out, Ly.s_out = enc(f"{mha}/attention_output", dims.d_p, dims.inner_p, kg=dk,
                                      kgp=dkp)
@@ -327,8 +348,13 @@ class Model:
             k_p = dims.d_p
             for j in range(kw["encoder_mlp_quantities"]):
                 n_p = dims.mlp_units_p[j]
-                Ly.w_mlp[j], Ly.s_mlp[j] = enc(f"MLP_{i}_{j + 1}", n_p, k_p)
-                Ly.b_mlp[j] = vector(f"MLP_{i}_{j + 1}/bias", n_p).data_ptr()
+                bm = vector(f"MLP_{i}_{j + 1}/bias", n_p)
+                if fold and j == 0:
+                    w32 = dense(f"MLP_{i}_{j + 1}", n_p, k_p, dst=f32_staging(n_p, k_p), pdt=L.F32)
+                    Ly.w_mlp[j], Ly.b_mlp[j], Ly.ln2_colsum = fold_ln(w32, bm, g2, b2)
+                else:
+                    Ly.w_mlp[j], Ly.s_mlp[j] = enc(f"MLP_{i}_{j + 1}", n_p, k_p)
+                    Ly.b_mlp[j] = bm.data_ptr()
                 k_p = n_p
         W.layers = ctypes.cast(layers, ctypes.POINTER(L.VtdLayerWeights))
         W.w_det = dense("dense", L.KALIGN, dims.d_p).data_ptr()
