@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define VTD_ABI_VERSION 4
+#define VTD_ABI_VERSION 5
 #define VTD_KALIGN 64          /* K / row padding granule, elements              */
 #define VTD_MAX_MLP 16         /* max encoder_mlp_quantities                     */
 #define VTD_MAX_HEAD 64        /* max mlp_head layers * repeats                   */
@@ -176,6 +176,11 @@ typedef struct vtd_epilogue {
    * (vtd_layernorm_stats) and colsum[n] = sum_k Bt[n][k]; the accumulator becomes
    * (acc - mean * colsum[n]) * rstd before bias / act.  Both NULL: no fold. */
   const float* lnstat; const float* colsum;
+  /* Partial LayerNorm statistics of the output (the fold path's producer side): for row m
+   * and 64-column block b, statout[2 (m stat_ld + b)] = sum and [.. + 1] = sum of squares
+   * of the stored bf16 values.  Only on full 256 x 256 tiles of the bf16 fast epilogues
+   * (else vtd_gemm returns VTD_ERR_UNSUPPORTED); NULL: none. */
+  float* statout; int stat_ld;
 } vtd_epilogue;
 int vtd_gemm(int M, int N, int K, const void* A_dev, int lda, const void* Bt_dev,
              int ldb, int dtype, const vtd_epilogue* epi, void* stream);
@@ -207,6 +212,11 @@ int vtd_layernorm(const void* x_dev, int x_dtype, int64_t rows, int D, int ldx,
  * first D columns of row r of x (x_dtype F32 or BF16). */
 int vtd_layernorm_stats(const void* x_dev, int x_dtype, int64_t rows, int D, int ldx,
                         float eps, float* stat_dev, void* stream);
+
+/* (mean, rstd) per row from the partial sums a producer GEMM wrote (vtd_epilogue.statout,
+ * `slots` 64-column blocks per row): one-pass variance sum(x^2)/D - mean^2 in fp32. */
+int vtd_layernorm_stats_finalize(const float* partial_dev, int64_t rows, int slots, int D,
+                                 float eps, float* stat_dev, void* stream);
 
 /* Folds LayerNorm(gamma, beta) into the Dense layer that consumes it: w32 fp32 packed
  * W^T [N][ldw] (first K columns used) -> w_out (dtype) [N][ldo] = W^T[n][k] * gamma[k]

@@ -454,3 +454,57 @@ def test_gemm_layernorm_fold(L, cuda, M, N, K, act, dtype):
     # the unfolded path has the same budget (h and W rounded to bf16).  f32: exact-ish.
     tol = 1.6e-2 if dtype == "bf16" else 1e-4
     assert err.max() < tol, err.max()
+
+
+@pytest.mark.parametrize("N,K,act,resid", [(768, 768, 0, True), (768, 1536, 1, True),
+                                           (1024, 512, 0, False), (512, 256, 2, False)])
+def test_gemm_statout_and_finalize(L, cuda, N, K, act, resid):
+    """Producer side of the LayerNorm fold: the bf16 fast epilogues (act 0: pp2b staged,
+    act > 0: transposed direct) emit per-(row, 64-column block) (sum, sum of squares) of
+    the STORED bf16 outputs; vtd_layernorm_stats_finalize turns them into (mean, rstd)."""
+    M = 256 * 64                       # >= 128 tiles: the 256-tile kernels
+    g = torch.Generator(device=cuda).manual_seed(N + K + act)
+    A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
+    Bt = (torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g, device=cuda)
+    x = (3 + 2 * torch.randn(M, N, generator=g, device=cuda)).to(torch.bfloat16)
+    slots = N // 64
+    part = torch.full((M, slots, 2), float("nan"), device=cuda)
+    e = L.VtdEpilogue()
+    e.bias, e.act, e.out, e.ldo, e.out_dtype = bias.data_ptr(), act, x.data_ptr(), N, 1
+    if resid:
+        e.resid, e.ldr = x.data_ptr(), N
+    e.statout, e.stat_ld = part.data_ptr(), slots
+    L.check(L.lib.vtd_gemm(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, L.BF16, ctypes.byref(e),
+                           L.stream_ptr()), "gemm")
+    st = torch.zeros(M, 2, device=cuda)
+    L.check(L.lib.vtd_layernorm_stats_finalize(part.data_ptr(), M, slots, N, 1e-3, st.data_ptr(),
+                                               L.stream_ptr()), "finalize")
+    torch.cuda.synchronize()
+    xs = x.double().cpu().numpy().reshape(M, slots, 64)
+    got = part.double().cpu().numpy()
+    np.testing.assert_allclose(got[..., 0], xs.sum(2), rtol=1e-5, atol=1e-4)
+    np.testing.assert_allclose(got[..., 1], (xs ** 2).sum(2), rtol=1e-5, atol=1e-4)
+    x64 = xs.reshape(M, N)
+    mu = x64.mean(1)
+    rstd = 1 / np.sqrt(x64.var(1) + 1e-3)
+    s = st.double().cpu().numpy()
+    assert np.abs(s[:, 0] - mu).max() < 1e-5 * max(1, np.abs(mu).max())
+    assert np.abs(s[:, 1] - rstd).max() < 1e-4 * rstd.max()
+
+
+def test_gemm_statout_unsupported_shape(L, cuda):
+    """statout only on full tiles: a ragged M is refused (the forward then runs the
+    row-statistics pass instead)."""
+    M, N, K = 256 * 64 + 8, 768, 256
+    A = torch.zeros(M, K, device=cuda, dtype=torch.bfloat16)
+    Bt = torch.zeros(N, K, device=cuda, dtype=torch.bfloat16)
+    out = torch.zeros(M, N, device=cuda, dtype=torch.bfloat16)
+    bias = torch.zeros(N, device=cuda)
+    part = torch.zeros(M, N // 64, 2, device=cuda)
+    e = L.VtdEpilogue()
+    e.bias, e.out, e.ldo, e.out_dtype = bias.data_ptr(), out.data_ptr(), N, 1
+    e.statout, e.stat_ld = part.data_ptr(), N // 64
+    with pytest.raises(L.VtdError):
+        L.check(L.lib.vtd_gemm(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, L.BF16, ctypes.byref(e),
+                               L.stream_ptr()), "gemm")

@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede loading libvtd.so, see module doc)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvtd.so")
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 KALIGN = 64
 MAX_MLP = 16
 MAX_HEAD = 64
@@ -72,7 +72,8 @@ class VtdEpilogue(ctypes.Structure):
         ("bias", c_void_p), ("rowadd", c_void_p), ("rowadd_period", c_int),
         ("rowadd_ncols", c_int), ("act", c_int), ("resid", c_void_p), ("ldr", c_int),
         ("out", c_void_p), ("ldo", c_int), ("out_dtype", c_int), ("out2", c_void_p),
-        ("ldo2", c_int), ("scatter_tokens", c_int), ("lnstat", c_void_p), ("colsum", c_void_p)]
+        ("ldo2", c_int), ("scatter_tokens", c_int), ("lnstat", c_void_p), ("colsum", c_void_p),
+        ("statout", c_void_p), ("stat_ld", c_int)]
 
 
 # name -> (restype, argtypes)
@@ -96,6 +97,8 @@ SIGNATURES = {
                               c_void_p, c_int, c_int, c_void_p]),
     "vtd_layernorm_stats": (c_int, [c_void_p, c_int, c_int64, c_int, c_int, c_float, c_void_p,
                                     c_void_p]),
+    "vtd_layernorm_stats_finalize": (c_int, [c_void_p, c_int64, c_int, c_int, c_float, c_void_p,
+                                             c_void_p]),
     "vtd_fold_layernorm": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "vtd_attention": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_float,

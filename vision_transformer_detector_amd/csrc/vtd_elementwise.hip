@@ -235,6 +235,25 @@ void ln_stats_dispatch(const void* xv, int64_t rows, int D, int ldx, float eps, 
 #undef VTD_LS
 }
 
+// (mean, rstd) per row from a producer GEMM's partial (sum, sum of squares) per 64-column
+// block: one thread per row.
+__global__ __launch_bounds__(256) void ln_stats_finalize_kernel(const float2* __restrict__ part,
+                                                                int64_t rows, int slots, int D,
+                                                                float eps,
+                                                                float2* __restrict__ stat) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= rows) return;
+  float s = 0.f, q = 0.f;
+  for (int b = 0; b < slots; ++b) {
+    const float2 t = part[r * slots + b];
+    s += t.x;
+    q += t.y;
+  }
+  const float mean = s / D;
+  const float var = fmaxf(q / D - mean * mean, 0.f);
+  stat[r] = float2{mean, 1.f / sqrtf(var + eps)};
+}
+
 // LayerNorm fold of one consumer Dense layer (one-time weight preparation): one wave per
 // output row n; fp64 sums (bias' from the fp32 W, colsum from the rounded stored W').
 template <typename TO>
@@ -399,6 +418,20 @@ int ln_stats_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx, fl
   return VTD_OK;
 }
 
+int ln_stats_finalize_launch(const float* part, int64_t rows, int slots, int D, float eps,
+                             float* stat, hipStream_t st) {
+  VTD_CHECK_ARG(part && stat, "layernorm_stats_finalize: null pointer");
+  VTD_CHECK_ARG(rows > 0 && slots > 0 && D > 0, "layernorm_stats_finalize: bad shape");
+  VTD_CHECK_ARG(reinterpret_cast<uintptr_t>(part) % 8 == 0 && reinterpret_cast<uintptr_t>(stat) % 8 == 0,
+                "layernorm_stats_finalize: alignment");
+  ProfScope ps(st, PROF_LN, 0.0);
+  hipLaunchKernelGGL(ln_stats_finalize_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0,
+                     st, reinterpret_cast<const float2*>(part), rows, slots, D, eps,
+                     reinterpret_cast<float2*>(stat));
+  VTD_LAUNCH_CHECK("layernorm_stats_finalize");
+  return VTD_OK;
+}
+
 int fold_ln_launch(const float* w, int N, int K, int ldw, const float* gamma, const float* beta,
                    const float* bias_in, void* wo, int ldo, int dtype, float* bias_out,
                    float* colsum, hipStream_t st) {
@@ -464,6 +497,12 @@ int vtd_layernorm_stats(const void* x_dev, int x_dtype, int64_t rows, int D, int
                         float eps, float* stat_dev, void* stream) {
   return vtd::ln_stats_launch(x_dev, x_dtype, rows, D, ldx, eps, stat_dev,
                               static_cast<hipStream_t>(stream));
+}
+
+int vtd_layernorm_stats_finalize(const float* partial_dev, int64_t rows, int slots, int D,
+                                 float eps, float* stat_dev, void* stream) {
+  return vtd::ln_stats_finalize_launch(partial_dev, rows, slots, D, eps, stat_dev,
+                                       static_cast<hipStream_t>(stream));
 }
 
 int vtd_fold_layernorm(const float* w32_dev, int N, int K, int ldw, const float* gamma_dev,

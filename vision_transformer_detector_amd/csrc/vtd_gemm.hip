@@ -36,7 +36,41 @@ struct EpiArgs {
   // LayerNorm folded into this GEMM (A = the raw residual stream): per row (mean, rstd),
   // per column colsum[n] = sum_k Bt[n][k]; acc -> (acc - mean * colsum) * rstd first
   const float2* lnstat; const float* colsum;
+  // partial LayerNorm statistics of the stored bf16 rows (fold path producer): per row m
+  // and 64-column block b, statout[m * stat_ld + b] = (sum, sum of squares)
+  float2* statout; int stat_ld;
 };
+
+// v of another lane of the same 16-lane row by a DPP control (0 where the source is out
+// of the row)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// v[l] + v[l ^ 16] and v[l] + v[l ^ 32] by the gfx950 lane-swap instructions (no LDS)
+__device__ __forceinline__ float xsum16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xsum32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// (sum, sum of squares) of the 8 bf16 values packed in o
+__device__ __forceinline__ float2 bf16x8_sums(const i32x4& o) {
+  float s = 0.f, q = 0.f;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const float lo = __uint_as_float((uint32_t)o[w] << 16);
+    const float hi = __uint_as_float((uint32_t)o[w] & 0xffff0000u);
+    s += lo + hi;
+    q += lo * lo + hi * hi;
+  }
+  return float2{s, q};
+}
 
 __device__ __forceinline__ float resid_at(const EpiArgs& e, int64_t i) {
   return e.out_dtype == VTD_F32 ? static_cast<const float*>(e.resid)[i]
@@ -519,6 +553,19 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
         const i32x4 o = {(int)pack_bf16x2(v0[0], v0[1]), (int)pack_bf16x2(v0[2], v0[3]),
                          (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
         *reinterpret_cast<i32x4*>(static_cast<bf16_t*>(e.out) + idx) = o;
+        if (e.statout) {           // the row's 64 columns live in 8 consecutive lanes
+          float2 t = bf16x8_sums(o);
+          // DPP sums (no LDS traffic): quad xor 1, quad xor 2, then row_shr 4 leaves the
+          // 8-lane total in lanes 4..7 of each 8-lane group
+          t.x += dpp_f32<0xB1>(t.x);
+          t.y += dpp_f32<0xB1>(t.y);
+          t.x += dpp_f32<0x4E>(t.x);
+          t.y += dpp_f32<0x4E>(t.y);
+          t.x += dpp_f32<0x114>(t.x);
+          t.y += dpp_f32<0x114>(t.y);
+          if ((lane & 7) == 7)
+            e.statout[(int64_t)(m_base + p * PR + row) * e.stat_ld + (n_base >> 6)] = t;
+        }
       } else {
         float* op = static_cast<float*>(e.out) + idx;
         *reinterpret_cast<f32x4*>(op) = v0;
@@ -902,7 +949,8 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
         }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {
+      float2 tsum = {0.f, 0.f};
 #pragma unroll
       for (int jp = 0; jp < 2; ++jp) {
         f32x4 v0 = acc[i0 + i][2 * jp];
@@ -928,12 +976,24 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
           const i32x4 o = {(int)pack_bf16x2(v0[0], v0[1]), (int)pack_bf16x2(v0[2], v0[3]),
                            (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
           *reinterpret_cast<i32x4*>(static_cast<bf16_t*>(e.out) + idx) = o;
+          if (e.statout) {
+            const float2 t = bf16x8_sums(o);
+            tsum.x += t.x;
+            tsum.y += t.y;
+          }
         } else {
           float* op = static_cast<float*>(e.out) + idx;
           *reinterpret_cast<f32x4*>(op) = v0;
           *reinterpret_cast<f32x4*>(op + 4) = v1;
         }
       }
+      if (OUT_BF16 && e.statout) {   // the row's 64 columns: lanes fr, fr + 16, + 32, + 48
+        tsum.x = xsum32(xsum16(tsum.x));
+        tsum.y = xsum32(xsum16(tsum.y));
+        if (fg == 0)
+          e.statout[(int64_t)(m_base + 16 * (i0 + i) + fr) * e.stat_ld + (n_base >> 6)] = tsum;
+      }
+    }
   }
 }
 
@@ -1574,6 +1634,33 @@ bool gemm_pp3_launch(int M, int N, int K, const bf16_t* A, int lda, const bf16_t
                      int ldb, const vtd_epilogue* epi, int code, int num_cu,
                      hipStream_t stream);
 
+// 10 = auto (default): 9 when the epilogue has an activation, else 8
+// 9 = 8 with transposed accumulators + register-direct epilogue;
+// 8 = ping-pong v2 with buffer-resource DMA; 6 = same with global_load_lds;
+// 7 = persistent v2; 1 = ping-pong v1; 4 = persistent; 0 = 2-barrier;
+// 11 = persistent pp3 (vtd_gemm_pp3.hip); 2, 3, 5 = timing diagnostics (wrong outputs)
+int gemm_variant() {
+  static const int variant = [] {
+    const char* v = getenv("VTD_GEMM_VARIANT");
+    return v ? atoi(v) : 10;
+  }();
+  return variant;
+}
+
+// Whether vtd_gemm can emit the partial LayerNorm statistics (epilogue.statout) for this
+// problem: every tile full and on the pp2b / pp2t fast epilogues with a bf16 output.
+bool gemm_emits_stats(int M, int N, int dtype, const vtd_epilogue* e) {
+  const int tiles = ((M + BBM - 1) / BBM) * ((N + BBN - 1) / BBN);
+  const int v = gemm_variant();
+  auto a16 = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
+  return dtype == VTD_BF16 && e->out_dtype == VTD_BF16 && tiles >= 128 && N > 64 &&
+         M % BBM == 0 && N % BBN == 0 && (v == 8 || v == 9 || v == 10) && e->bias &&
+         e->scatter_tokens <= 0 && e->ldo % 8 == 0 && a16(e->out) && a16(e->bias) &&
+         (!e->resid || (e->ldr % 8 == 0 && a16(e->resid))) &&
+         (!e->out2 || (e->ldo2 % 8 == 0 && a16(e->out2))) && e->stat_ld >= N / 64 &&
+         reinterpret_cast<uintptr_t>(e->statout) % 8 == 0;
+}
+
 int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
                 int dtype, const vtd_epilogue* epi, hipStream_t stream, double flops) {
   VTD_CHECK_ARG(M > 0 && N > 0 && K > 0, "gemm: M, N, K must be positive");
@@ -1590,10 +1677,14 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
   VTD_CHECK_ARG(!epi->lnstat || (epi->colsum && reinterpret_cast<uintptr_t>(epi->lnstat) % 8 == 0 &&
                                  reinterpret_cast<uintptr_t>(epi->colsum) % 16 == 0),
                 "gemm: lnstat needs colsum (16-B aligned) and 8-B alignment");
+  if (epi->statout && !gemm_emits_stats(M, N, dtype, epi))
+    return fail(VTD_ERR_UNSUPPORTED, "gemm: statout needs full 256 x 256 tiles on the bf16 "
+                                     "fast epilogues (see gemm_emits_stats)");
   EpiArgs e{epi->bias, epi->rowadd, epi->rowadd_period,
             epi->rowadd ? epi->rowadd_ncols : 0, epi->act, epi->resid, epi->ldr,
             epi->out, epi->ldo, epi->out_dtype, epi->out2, epi->ldo2,
-            epi->scatter_tokens, reinterpret_cast<const float2*>(epi->lnstat), epi->colsum};
+            epi->scatter_tokens, reinterpret_cast<const float2*>(epi->lnstat), epi->colsum,
+            reinterpret_cast<float2*>(epi->statout), epi->stat_ld};
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM);
   const size_t lds = 4 * TILE_BYTES;
   ProfScope ps(stream, PROF_GEMM, flops > 0 ? flops : 2.0 * M * N * (double)K);
@@ -1627,15 +1718,7 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
                                   2 * BSTAGE + EPR_BYTES);
       attr = true;
     }
-    // 10 = auto (default): 9 when the epilogue has an activation, else 8
-    // 9 = 8 with transposed accumulators + register-direct epilogue;
-    // 8 = ping-pong v2 with buffer-resource DMA; 6 = same with global_load_lds;
-    // 7 = persistent v2; 1 = ping-pong v1; 4 = persistent; 0 = 2-barrier;
-    // 2, 3, 5 = timing diagnostics (wrong outputs)
-    static const int variant = [] {
-      const char* v = getenv("VTD_GEMM_VARIANT");
-      return v ? atoi(v) : 10;
-    }();
+    const int variant = gemm_variant();
     const dim3 g(tiles_m * tiles_n), b(BNT);
     const bf16_t* a16 = static_cast<const bf16_t*>(A);
     const bf16_t* b16 = static_cast<const bf16_t*>(Bt);
@@ -1767,10 +1850,12 @@ int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_
   VTD_CHECK_ARG(!epi->lnstat || (epi->colsum && reinterpret_cast<uintptr_t>(epi->lnstat) % 8 == 0 &&
                                  reinterpret_cast<uintptr_t>(epi->colsum) % 16 == 0),
                 "gemm_mx8: lnstat needs colsum (16-B aligned) and 8-B alignment");
+  if (epi->statout) return fail(VTD_ERR_UNSUPPORTED, "gemm_mx8: statout is not supported");
   EpiArgs e{epi->bias, epi->rowadd, epi->rowadd_period,
             epi->rowadd ? epi->rowadd_ncols : 0, epi->act, epi->resid, epi->ldr,
             epi->out, epi->ldo, epi->out_dtype, epi->out2, epi->ldo2,
-            epi->scatter_tokens, reinterpret_cast<const float2*>(epi->lnstat), epi->colsum};
+            epi->scatter_tokens, reinterpret_cast<const float2*>(epi->lnstat), epi->colsum,
+            reinterpret_cast<float2*>(epi->statout), epi->stat_ld};
   ProfScope ps(stream, PROF_GEMM, flops > 0 ? flops : 2.0 * M * N * (double)K);
   const int tiles_m = (M + BBM - 1) / BBM, tiles_n = (N + BBN - 1) / BBN;
   static bool attr = false;

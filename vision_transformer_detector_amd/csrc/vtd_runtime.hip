@@ -19,6 +19,9 @@ int layernorm_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx, c
                      const float* b, float eps, void* y, int ldy, int dtype, hipStream_t st);
 int ln_stats_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx, float eps,
                     float* stat, hipStream_t st);
+int ln_stats_finalize_launch(const float* part, int64_t rows, int slots, int D, float eps,
+                             float* stat, hipStream_t st);
+bool gemm_emits_stats(int M, int N, int dtype, const vtd_epilogue* e);
 int patches_launch(const float* img, int B, int H, int W, int C, int p, void* out, int ldo,
                    int dtype, hipStream_t st);
 int decode_launch(const float* logits, int64_t n, float* dets, hipStream_t st);
@@ -139,7 +142,7 @@ static int derive(const vtd_config* c, vtd_dims* d) {
 
 namespace {
 struct Plan {
-  size_t patches, x, xb, h, stat, qkv, attn, mlp0, mlp1, u, head0, head1, q8, s8, total;
+  size_t patches, x, xb, h, stat, pstat, qkv, attn, mlp0, mlp1, u, head0, head1, q8, s8, total;
   int k8_max;                       // widest MX-fp8 GEMM K (VTD_FP8)
   int64_t s8_rows;                  // activation scale rows (rows rounded up to 4)
 };
@@ -175,6 +178,7 @@ Plan make_plan(const vtd_config* c, const vtd_dims& d) {
   p.xb = take(act_dtype(c->dtype) == VTD_BF16 ? R * d.d_p * 2 : 0);
   p.h = take(R * d.d_p * es);
   p.stat = take(R * 8);                 // LayerNorm (mean, rstd) per row, fold path
+  p.pstat = take(R * (d.d_p / 64) * 8);  // producer partial (sum, sumsq) per 64 columns
   p.qkv = take(R * d.qkv_p * es);
   p.attn = take(R * d.inner_p * es);
   p.mlp0 = take(R * mlp_max * es);
@@ -240,6 +244,26 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
   const int rdt = resid_dtype(cfg->dtype);
   float* stat = reinterpret_cast<float*>(ws + P.stat);
   void* x = ws + P.x;
+  float* pstat = reinterpret_cast<float*>(ws + P.pstat);
+  const int nslot = Dp / 64;
+  // fold path: the GEMM writing x emits partial row statistics when it can (full tiles on
+  // the bf16 fast epilogues); the LayerNorm point then only finalizes them
+  bool partials = false;
+  static const bool partials_on = [] {       // VTD_LN_PARTIALS=0: row-statistics pass
+    const char* v = getenv("VTD_LN_PARTIALS");
+    return !v || atoi(v) != 0;
+  }();
+  auto emit_stats = [&](vtd_epilogue& e, bool next_fold) {
+    partials = false;
+    if (!next_fold || fp8 || dt != VTD_BF16 || !partials_on) return;
+    e.statout = pstat; e.stat_ld = nslot;
+    partials = gemm_emits_stats(M, Dp, dt, &e);
+    if (!partials) { e.statout = nullptr; e.stat_ld = 0; }
+  };
+  auto row_stats = [&]() -> int {
+    return partials ? ln_stats_finalize_launch(pstat, R, nslot, D, 1e-3f, stat, st)
+                    : ln_stats_launch(x, rdt, R, D, Dp, 1e-3f, stat, st);
+  };
   void* xb = ws + P.xb;
   void* h = ws + P.h;
   void* qkv = ws + P.qkv;
@@ -275,6 +299,7 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
     e.rowadd = w->pos_embedding; e.rowadd_period = N; e.rowadd_ncols = D;
     e.act = VTD_ACT_NONE;
     e.out = x; e.ldo = Dp; e.out_dtype = rdt;
+    emit_stats(e, cfg->repeat_times > 0 && w->layers[0].ln1_colsum);
     rc = gemm_launch(M, Dp, d.patch_dim_p, patches, d.patch_dim_p, w->w_patch,
                      d.patch_dim_p, dt, &e, st, 2.0 * fR * D * d.patch_dim);
     if (rc) return rc;
@@ -288,7 +313,7 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
     // LayerNorm 1: its own pass into h, or folded into the query/key/value GEMM
     const void* a1 = h;
     if (L.ln1_colsum) {
-      rc = ln_stats_launch(x, rdt, R, D, Dp, 1e-3f, stat, st);
+      rc = row_stats();
       a1 = x;
     } else {
       rc = layernorm_launch(x, rdt, R, D, Dp, L.ln1_gamma, L.ln1_beta, 1e-3f, h, Dp, dt, st);
@@ -312,13 +337,14 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
       e.bias = L.b_out; e.act = VTD_ACT_NONE;
       e.resid = x; e.ldr = Dp;
       e.out = x; e.ldo = Dp; e.out_dtype = rdt;
+      emit_stats(e, L.ln2_colsum != nullptr);
       rc = enc_gemm(Dp, d.inner_p, attn, L.w_out, L.s_out, &e,
                     2.0 * fR * cfg->num_heads * cfg->key_dim * D);
       if (rc) return rc;
     }
     const void* a = h;
     if (L.ln2_colsum) {
-      rc = ln_stats_launch(x, rdt, R, D, Dp, 1e-3f, stat, st);
+      rc = row_stats();
       a = x;
     } else {
       rc = layernorm_launch(x, rdt, R, D, Dp, L.ln2_gamma, L.ln2_beta, 1e-3f, h, Dp, dt, st);
@@ -336,6 +362,7 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
         if (i == cfg->repeat_times - 1 && dt == VTD_BF16 && rdt == VTD_F32) {
           e.out2 = xb; e.ldo2 = Dp;           // bf16 copy of an f32 stream for the head
         }
+        emit_stats(e, i + 1 < cfg->repeat_times && w->layers[i + 1].ln1_colsum);
       } else {
         e.out = mlp[j & 1]; e.ldo = d.mlp_units_p[j]; e.out_dtype = dt;
       }
