@@ -132,8 +132,11 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32", "fp8"])
     ap.add_argument("--preset", default="vit_b16_224")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="vtd_forward micro-batch streams (VTD_STREAMS; 1 = one stream)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
+    os.environ["VTD_STREAMS"] = str(args.streams)      # read once by libvtd.so
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -183,7 +186,10 @@ def main():
         elapsed = float(t.item())
 
     # ---- per-kernel timing: hipEvents recorded around every launch of vtd_forward on
-    # the stream it launches on, over K more steps of the same workload
+    # the stream it launches on, over K more steps of the same workload.  Profiling runs
+    # vtd_forward on one stream (no micro-batch overlap), so each launch's event pair
+    # times that kernel alone: the roofline below is the kernel's own, while `value`
+    # (the timed region above) includes the two-stream overlap.
     L.check(L.lib.vtd_profile_reset())
     L.check(L.lib.vtd_profile_enable(1))
     torch.cuda.synchronize()
@@ -227,7 +233,7 @@ def main():
         "config": {"workload": f"{args.preset} detector forward + decode + all-gather of "
                                f"detections", "per_gpu_batch": B, "global_batch": world * B,
                    "input_shape": list(shape), "tokens": model.dims.tokens,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}", "streams_per_gpu": args.streams},
         "mfma_util_attn_mlp": round(attn_mlp_fl * img_s / world / (peak * 1e12), 4),
         "model_tflops_per_gpu": round(total_fl * img_s / world / 1e12, 1),
         "roofline": {"bound": "mfma",

@@ -148,3 +148,48 @@ def test_weight_file_round_trip(vtd, cuda, tmp_path, ext):
     m2.load_weights(path)
     xb = torch.from_numpy(x).to(cuda)
     assert torch.equal(m1(xb), m2(xb))
+
+
+SPLIT_KW = dict(input_shape=(224, 224, 3), patch_size=16, embedding_dim=64, encoder_num_heads=2,
+                encoder_key_dim=32, encoder_mlp_quantities=2, encoder_repeat_times=2,
+                mlp_head_last_units=8, mlp_head_dense_layers_quantity=2)
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_two_stream_split_matches_single_images(vtd, cuda, dtype):
+    """A batch large enough for vtd_forward's two-stream micro-batching (128 x 196 rows:
+    the halves run on the caller's stream and an internal second stream) gives each image
+    the result it gets alone: bit-exact in float32 (one GEMM kernel for every M), within
+    the bf16 tolerance against a single-image forward in bfloat16 (the 256-tile kernels
+    only serve the large batch)."""
+    model = vtd.create_vision_transformer_detector(**SPLIT_KW, dtype=dtype, seed=3)
+    g = torch.Generator(device=cuda).manual_seed(1)
+    x = torch.rand(128, 224, 224, 3, generator=g, device=cuda) * 2 - 1
+    full = model(x)
+    torch.cuda.synchronize()
+    for i in (0, 63, 64, 127):                  # both halves, both edges
+        one = model(x[i:i + 1])
+        if dtype == "float32":
+            assert torch.equal(one[0], full[i]), i
+        else:
+            ok, rel = within(full[i].cpu().numpy(), one[0].cpu().numpy(), TOL[dtype])
+            assert ok, (i, rel)
+
+
+def test_two_stream_split_graph_capture(vtd, cuda):
+    """The split forward (fork / join events to the internal stream) is HIP-graph
+    capturable: the replay reproduces the eager result exactly."""
+    model = vtd.create_vision_transformer_detector(**SPLIT_KW, dtype="bfloat16", seed=4)
+    g = torch.Generator(device=cuda).manual_seed(2)
+    x = torch.rand(128, 224, 224, 3, generator=g, device=cuda) * 2 - 1
+    eager = model(x).clone()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        model(x)
+        graph = torch.cuda.CUDAGraph()
+        buf = torch.empty_like(eager)
+        with torch.cuda.graph(graph, stream=s):
+            buf.copy_(model.forward(x))
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(buf, eager)

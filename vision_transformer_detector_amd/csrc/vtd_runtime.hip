@@ -198,6 +198,73 @@ Plan make_plan(const vtd_config* c, const vtd_dims& d) {
   p.total = off;
   return p;
 }
+// Two-stream micro-batching of vtd_forward: the images are independent, so a large
+// batch is run as two halves on the caller's stream and an internal second stream.  The
+// halves' kernels co-run, so the last partial round of one half's GEMM tiles (e.g. 588
+// tiles of an N = 768 layer = 2.3 rounds of 256 CUs) runs beside the other half's work
+// instead of leaving CUs idle.  VTD_STREAMS=1 disables it; so does per-kernel profiling
+// (vtd_profile_enable): each profiled launch then runs alone and its events time it.
+int split_count(const vtd_config* c, const vtd_dims& d) {
+  if (prof().enabled) return 1;
+  static const int streams = [] {
+    const char* v = getenv("VTD_STREAMS");
+    return v ? atoi(v) : 2;
+  }();
+  // only where each half still has >= 48 row tiles of 256 (C2 at B = 256: 98 each)
+  return streams >= 2 && c->batch >= 2 && d.rows >= (int64_t)2 * 48 * 256 ? 2 : 1;
+}
+vtd_config sub_config(const vtd_config* c, int part, int nsplit) {
+  vtd_config s = *c;
+  const int b0 = c->batch / nsplit;
+  s.batch = part == nsplit - 1 ? c->batch - b0 * (nsplit - 1) : b0;
+  return s;
+}
+// workspace of either form (profiling can toggle between them)
+size_t split_workspace(const vtd_config* c, const vtd_dims& d) {
+  const size_t whole = make_plan(c, d).total;
+  static const int streams = [] {
+    const char* v = getenv("VTD_STREAMS");
+    return v ? atoi(v) : 2;
+  }();
+  const int ns = streams >= 2 && c->batch >= 2 ? 2 : 1;
+  if (ns == 1) return whole;
+  size_t total = 0;
+  for (int i = 0; i < ns; ++i) {
+    const vtd_config sc = sub_config(c, i, ns);
+    vtd_dims sd;
+    if (derive(&sc, &sd) != VTD_OK) return 0;
+    total += make_plan(&sc, sd).total;
+  }
+  return std::max(total, whole);
+}
+struct SideStream {
+  int device = -1;
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+// per-device side stream + fork/join events, created on the first eager call (never
+// during a HIP-graph capture: a captured first call runs unsplit)
+SideStream* side_stream(hipStream_t st) {
+  static std::mutex mu;
+  static SideStream per_dev[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  SideStream& ss = per_dev[dev];
+  if (ss.s) return &ss;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+    return nullptr;
+  if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+  if (hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess)
+    return nullptr;
+  ss.device = dev;
+  return &ss;
+}
+
+int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* images,
+                 float* logits, float* dets, char* ws, hipStream_t st);
 }  // namespace
 
 }  // namespace vtd
@@ -216,8 +283,8 @@ int vtd_workspace_bytes(const vtd_config* cfg, size_t* bytes) {
   vtd_dims d;
   int rc = derive(cfg, &d);
   if (rc) return rc;
-  *bytes = make_plan(cfg, d).total;
-  return VTD_OK;
+  *bytes = split_workspace(cfg, d);
+  return *bytes ? VTD_OK : fail(VTD_ERR_INVALID_ARG, "workspace: bad split config");
 }
 
 int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images,
@@ -228,12 +295,51 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
   if (rc) return rc;
   VTD_CHECK_ARG(w && images && logits && workspace, "forward: null pointer");
   VTD_CHECK_ARG(w->layers, "forward: weights.layers is null");
-  const Plan P = make_plan(cfg, d);
-  if (workspace_bytes < P.total)
+  const size_t need = split_workspace(cfg, d);
+  if (workspace_bytes < need)
     return fail(VTD_ERR_WORKSPACE, "forward: workspace too small (need " +
-                                       std::to_string(P.total) + " bytes)");
+                                       std::to_string(need) + " bytes)");
   hipStream_t st = static_cast<hipStream_t>(stream_);
   char* ws = static_cast<char*>(workspace);
+  const int ns = split_count(cfg, d);
+  SideStream* side = ns > 1 ? side_stream(st) : nullptr;
+  if (!side) {
+    if (ns == 1) return forward_impl(cfg, w, images, logits, dets, ws, st);
+    // no side stream (first call under capture): the halves run in order on `st`
+  }
+  const vtd_config c0 = sub_config(cfg, 0, 2), c1 = sub_config(cfg, 1, 2);
+  vtd_dims d0;
+  rc = derive(&c0, &d0);
+  if (rc) return rc;
+  const size_t img = (size_t)cfg->image_h * cfg->image_w * cfg->channels;
+  const size_t out0 = (size_t)c0.batch * VTD_MAX_DETECT * 6;
+  hipStream_t s1 = st;
+  if (side) {
+    VTD_HIP(hipEventRecord(side->fork, st));
+    VTD_HIP(hipStreamWaitEvent(side->s, side->fork, 0));
+    s1 = side->s;
+  }
+  rc = forward_impl(&c0, w, images, logits, dets, ws, st);
+  if (rc) return rc;
+  rc = forward_impl(&c1, w, images + c0.batch * img, logits + out0, dets ? dets + out0 : nullptr,
+                    ws + make_plan(&c0, d0).total, s1);
+  if (rc) return rc;
+  if (side) {
+    VTD_HIP(hipEventRecord(side->join, side->s));
+    VTD_HIP(hipStreamWaitEvent(st, side->join, 0));
+  }
+  return VTD_OK;
+}
+}  // extern "C"
+
+namespace vtd {
+namespace {
+int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* images,
+                 float* logits, float* dets, char* ws, hipStream_t st) {
+  vtd_dims d;
+  int rc = derive(cfg, &d);
+  if (rc) return rc;
+  const Plan P = make_plan(cfg, d);
   const bool fp8 = cfg->dtype == VTD_FP8;
   const int dt = act_dtype(cfg->dtype);
   const int B = cfg->batch, N = d.tokens, D = d.d, Dp = d.d_p;
@@ -414,6 +520,10 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
   }
   return VTD_OK;
 }
+}  // namespace
+}  // namespace vtd
+
+extern "C" {
 
 int vtd_profile_enable(int enable) {
   ProfState& p = prof();
