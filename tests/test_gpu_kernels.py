@@ -230,8 +230,10 @@ def test_attention_uniform_kat(L, cuda):
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("H,W,p", [(5, 5, 2), (608, 608, 17), (224, 224, 16), (40, 36, 8),
-                                   (13, 7, 4)])
+                                   (13, 7, 4), (384, 384, 16), (64, 32, 8)])
 def test_extract_patches(L, cuda, dtype, H, W, p):
+    """Generic gather kernel and (unpadded, bf16, P % 64 == 0: 224/16, 384/16, 64x32/8)
+    the row-segment copy kernel."""
     code, tdt = _dt(L, dtype)
     B, C = 2, 3
     img = ref.synthetic_images(B, (H, W, C), seed=H + W)

@@ -330,6 +330,31 @@ __global__ __launch_bounds__(256) void patches_kernel(
   }
 }
 
+// Unpadded case (H, W multiples of p; p*C % 8 == 0; ld_out == P), bf16 out: a patch row
+// kh of token m is p*C consecutive floats of image row gy*p + kh, so each thread moves 8
+// consecutive floats (two 16-B loads) to one 16-B store with no index arithmetic per
+// element.  Same output as patches_kernel.
+__global__ __launch_bounds__(256) void patches_dense_kernel(
+    const float* __restrict__ img, int64_t total, int H, int W, int C, int p, int gw, int N,
+    bf16_t* __restrict__ out) {
+  const int seg = p * C / 8;                 // 8-float chunks per patch row
+  const int per_tok = p * seg;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = g / per_tok;
+    const int r = (int)(g - m * per_tok);
+    const int kh = r / seg, c8 = r - kh * seg;
+    const int b = (int)(m / N), t = (int)(m - (int64_t)b * N);
+    const int gy = t / gw, gx = t - gy * gw;
+    const float* src = img + (((int64_t)b * H + gy * p + kh) * W + gx * p) * C + c8 * 8;
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(src);
+    const f32x4 v1 = *reinterpret_cast<const f32x4*>(src + 4);
+    const uint4 o = {pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3]),
+                     pack_bf16x2(v1[0], v1[1]), pack_bf16x2(v1[2], v1[3])};
+    *reinterpret_cast<uint4*>(out + m * (int64_t)(p * p * C) + kh * p * C + c8 * 8) = o;
+  }
+}
+
 // ------------------------------------------------------------------ decode
 // transform_predictions (vtd.py:586-647): sigmoid; clip last 4 to [0, 1];
 // [conf, cls * (CLASSES-1), cx * W, cy * H, h * H, w * W] with W = H = 608 (constant
@@ -462,7 +487,14 @@ int patches_launch(const float* img, int B, int H, int W, int C, int p, void* ou
   const int64_t total = (int64_t)B * N * (ldo / 8);
   const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
   ProfScope ps(st, PROF_PATCH, 0.0);
-  if (dtype == VTD_BF16)
+  if (dtype == VTD_BF16 && pad_h == 0 && pad_w == 0 && (p * C) % 8 == 0 && ldo == P &&
+      (W * C) % 4 == 0 && reinterpret_cast<uintptr_t>(img) % 16 == 0 &&
+      reinterpret_cast<uintptr_t>(out) % 16 == 0) {
+    const int64_t tot = (int64_t)B * N * P / 8;
+    const int gd = (int)std::min<int64_t>((tot + 255) / 256, 16384);
+    hipLaunchKernelGGL(patches_dense_kernel, dim3(gd), dim3(256), 0, st, img, tot, H, W, C, p,
+                       gw, N, static_cast<bf16_t*>(out));
+  } else if (dtype == VTD_BF16)
     hipLaunchKernelGGL(patches_kernel<bf16_t>, dim3(grid), dim3(256), 0, st, img, B, H, W,
                        C, p, gw, N, pad_h / 2, pad_w / 2, P, static_cast<bf16_t*>(out), ldo);
   else
