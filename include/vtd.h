@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define VTD_ABI_VERSION 5
+#define VTD_ABI_VERSION 6
 #define VTD_KALIGN 64          /* K / row padding granule, elements              */
 #define VTD_MAX_MLP 16         /* max encoder_mlp_quantities                     */
 #define VTD_MAX_HEAD 64        /* max mlp_head layers * repeats                   */
@@ -181,6 +181,11 @@ typedef struct vtd_epilogue {
    * of the stored bf16 values.  Only on full 256 x 256 tiles of the bf16 fast epilogues
    * (else vtd_gemm returns VTD_ERR_UNSUPPORTED); NULL: none. */
   float* statout; int stat_ld;
+  /* out_dtype VTD_FP8 (vtd_gemm_mx8 only, every tile full: M % 256 == N % 256 == 0): the
+   * output is written as the next GEMM's MX-fp8 A operand, byte for byte what
+   * vtd_quantize_mx8 makes of the bf16-rounded output: e4m3 out[m * ldo + n] and
+   * scale_out[n/128][scale_rows][4]. */
+  uint8_t* scale_out; int64_t scale_rows;
 } vtd_epilogue;
 int vtd_gemm(int M, int N, int K, const void* A_dev, int lda, const void* Bt_dev,
              int ldb, int dtype, const vtd_epilogue* epi, void* stream);
@@ -196,6 +201,11 @@ int vtd_gemm(int M, int N, int K, const void* A_dev, int lda, const void* Bt_dev
  * D = sum_k dec(A) dec(Bt) accumulated in fp32 by v_mfma_scale_f32_16x16x128_f8f6f4. */
 int vtd_quantize_mx8(const void* x_dev, int x_dtype, int64_t rows, int K, int ldx, int Kq,
                      uint8_t* q_dev, int ldq, uint8_t* s_dev, int64_t s_rows, void* stream);
+/* vtd_layernorm with the output quantized as vtd_quantize_mx8 does the bf16-rounded
+ * LayerNorm output (Kq % 128 == 0 >= D columns, ldq % 16 == 0): LN + quantize in one pass. */
+int vtd_layernorm_mx8(const void* x_dev, int x_dtype, int64_t rows, int D, int ldx,
+                      const float* gamma_dev, const float* beta_dev, float eps, uint8_t* q_dev,
+                      int ldq, int Kq, uint8_t* s_dev, int64_t s_rows, void* stream);
 int vtd_gemm_mx8(int M, int N, int K, const uint8_t* A_dev, int lda, const uint8_t* sA_dev,
                  int64_t sa_rows, const uint8_t* Bt_dev, int ldb, const uint8_t* sB_dev,
                  int64_t sb_rows, const vtd_epilogue* epi, void* stream);

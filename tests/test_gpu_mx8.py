@@ -96,3 +96,61 @@ def test_gemm_mx8_matches_dequantized_fp64(L, cuda, M, N, K, act, out_dtype, res
     tol = 5e-4 if out_dtype == 0 else 8e-3
     err = np.abs(got - ref64) / np.maximum(np.abs(ref64), 1.0)
     assert err.max() < tol, (err.max(), np.argwhere(err >= tol)[:5].tolist())
+
+
+@pytest.mark.parametrize("rows,D,x_dtype", [(200, 768, "bf16"), (64, 1024, "f32"), (37, 96, "bf16")])
+def test_layernorm_mx8_equals_layernorm_then_quantize(L, cuda, rows, D, x_dtype):
+    """The fused LayerNorm -> MX-fp8 pass writes exactly the bytes of vtd_layernorm (bf16 out)
+    followed by vtd_quantize_mx8."""
+    g = torch.Generator(device=cuda).manual_seed(rows + D)
+    xdt = torch.bfloat16 if x_dtype == "bf16" else torch.float32
+    x = (torch.randn(rows, D, generator=g, device=cuda) * 3 + 1).to(xdt)
+    gamma = 1 + 0.2 * torch.randn(D, generator=g, device=cuda)
+    beta = 0.3 * torch.randn(D, generator=g, device=cuda)
+    xc = L.BF16 if x_dtype == "bf16" else L.F32
+    Kq = -(-D // 128) * 128
+    h = torch.zeros(rows, D, device=cuda, dtype=torch.bfloat16)
+    L.check(L.lib.vtd_layernorm(x.data_ptr(), xc, rows, D, D, gamma.data_ptr(), beta.data_ptr(),
+                                1e-3, h.data_ptr(), D, L.BF16, L.stream_ptr()), "ln")
+    q_ref, s_ref, s_rows = _quantize(L, h, Kq)
+    q = torch.full((rows, Kq), 0x7f, dtype=torch.uint8, device=cuda)
+    s = torch.full_like(s_ref, 0xff)
+    L.check(L.lib.vtd_layernorm_mx8(x.data_ptr(), xc, rows, D, D, gamma.data_ptr(),
+                                    beta.data_ptr(), 1e-3, q.data_ptr(), Kq, Kq, s.data_ptr(),
+                                    s_rows, L.stream_ptr()), "ln_mx8")
+    torch.cuda.synchronize()
+    assert torch.equal(q, q_ref)
+    s_ref_v = s_ref.view(Kq // 128, s_rows, 4)[:, :rows]
+    assert torch.equal(s.view(Kq // 128, s_rows, 4)[:, :rows], s_ref_v)
+
+
+@pytest.mark.parametrize("M,N,K,act", [(4096, 1024, 1024, 1), (2560, 512, 384, 0)])
+def test_gemm_mx8_fp8_output_equals_quantized_bf16_output(L, cuda, M, N, K, act):
+    """out_dtype VTD_FP8 (the next MX GEMM's operand written by the epilogue) equals the bf16
+    output of the same GEMM passed through vtd_quantize_mx8, byte for byte."""
+    g = torch.Generator(device=cuda).manual_seed(M + N + K + 7)
+    A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
+    W = torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)
+    qa, sa, sa_rows = _quantize(L, A, K)
+    qb, sb, sb_rows = _quantize(L, W, K)
+    bias = torch.randn(N, generator=g, device=cuda)
+    out = torch.zeros(M, N, device=cuda, dtype=torch.bfloat16)
+
+    def run(e):
+        L.check(L.lib.vtd_gemm_mx8(M, N, K, qa.data_ptr(), K, sa.data_ptr(), sa_rows,
+                                   qb.data_ptr(), K, sb.data_ptr(), sb_rows, ctypes.byref(e),
+                                   L.stream_ptr()), "gemm_mx8")
+
+    e = L.VtdEpilogue()
+    e.bias, e.act, e.out, e.ldo, e.out_dtype = bias.data_ptr(), act, out.data_ptr(), N, 1
+    run(e)
+    q_ref, s_ref, s_rows = _quantize(L, out, N)
+    q = torch.full((M, N), 0x7f, dtype=torch.uint8, device=cuda)
+    s = torch.full_like(s_ref, 0xff)
+    e2 = L.VtdEpilogue()
+    e2.bias, e2.act, e2.out, e2.ldo, e2.out_dtype = bias.data_ptr(), act, q.data_ptr(), N, 2
+    e2.scale_out, e2.scale_rows = s.data_ptr(), s_rows
+    run(e2)
+    torch.cuda.synchronize()
+    assert torch.equal(q, q_ref)
+    assert torch.equal(s, s_ref)

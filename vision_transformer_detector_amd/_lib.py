@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede loading libvtd.so, see module doc)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvtd.so")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 KALIGN = 64
 MAX_MLP = 16
 MAX_HEAD = 64
@@ -73,7 +73,8 @@ class VtdEpilogue(ctypes.Structure):
         ("rowadd_ncols", c_int), ("act", c_int), ("resid", c_void_p), ("ldr", c_int),
         ("out", c_void_p), ("ldo", c_int), ("out_dtype", c_int), ("out2", c_void_p),
         ("ldo2", c_int), ("scatter_tokens", c_int), ("lnstat", c_void_p), ("colsum", c_void_p),
-        ("statout", c_void_p), ("stat_ld", c_int)]
+        ("statout", c_void_p), ("stat_ld", c_int), ("scale_out", c_void_p),
+        ("scale_rows", c_int64)]
 
 
 # name -> (restype, argtypes)
@@ -91,6 +92,8 @@ SIGNATURES = {
                          ctypes.POINTER(VtdEpilogue), c_void_p]),
     "vtd_quantize_mx8": (c_int, [c_void_p, c_int, c_int64, c_int, c_int, c_int, c_void_p, c_int,
                                  c_void_p, c_int64, c_void_p]),
+    "vtd_layernorm_mx8": (c_int, [c_void_p, c_int, c_int64, c_int, c_int, c_void_p, c_void_p,
+                                  c_float, c_void_p, c_int, c_int, c_void_p, c_int64, c_void_p]),
     "vtd_gemm_mx8": (c_int, [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int64, c_void_p,
                              c_int, c_void_p, c_int64, ctypes.POINTER(VtdEpilogue), c_void_p]),
     "vtd_layernorm": (c_int, [c_void_p, c_int, c_int64, c_int, c_int, c_void_p, c_void_p, c_float,

@@ -77,6 +77,28 @@ template <> struct DT<bf16_t> {
   __device__ static bf16_t from(float v) { return f32_to_bf16(v); }
 };
 
+// ----------------------------------------------------------------- MX-fp8 (vtd_mx8.hip)
+// E8M0 block exponent: the least E with amax <= 448 * 2^E (e4m3 max 448), clamped to
+// [-126, 126]; amax = m 2^ex (m in [0.5, 1)) gives E = ex - 9 + (m > 0.875) (oracle/mx8.py).
+__device__ __forceinline__ int mx8_exponent(float amax) {
+  const uint32_t b = __float_as_uint(amax);
+  const int e = (int)((b >> 23) & 0xff);
+  if (e == 0) return -126;                           // zero / subnormal block
+  const int E = e - 126 - 9 + ((b & 0x7fffff) > 0x600000 ? 1 : 0);
+  return min(max(E, -126), 126);
+}
+// 4 values * inv (= 2^-E, exact) -> 4 e4m3 bytes (round to nearest even), little-endian
+__device__ __forceinline__ uint32_t mx8_pack4(float a, float b, float c, float d, float inv) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a * inv, b * inv, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c * inv, d * inv, w, true);
+  return (uint32_t)w;
+}
+// bf16 rounding of an f32 value, back in f32 (the fused quantizers quantize what the
+// unfused path would have stored as bf16)
+__device__ __forceinline__ float bf16_round(float v) {
+  return __uint_as_float((uint32_t)f32_to_bf16(v) << 16);
+}
+
 // ----------------------------------------------------------------- activations
 // tfa.activations.mish = x * tanh(softplus(x)) (vtd.py:128-129).
 // tanh(log(1+e^x)) = n / (n + 2) with n = e^x (e^x + 2): no cancellation for x << 0.

@@ -127,6 +127,72 @@ int ln_dispatch(const void* xv, int64_t rows, int D, int ldx, const float* g,
   return VTD_OK;
 }
 
+// LayerNorm with the output quantized to MX-fp8 (VTD_FP8 mode: the next GEMM's A operand
+// without a bf16 round trip through HBM).  Same statistics as layernorm_kernel; each lane
+// owns 4 consecutive columns, so a 32-column block is 8 consecutive lanes: block amax by
+// DPP (quad xor 1, xor 2) + one lane ^ 4 exchange; values are bf16-rounded first so the
+// bytes equal vtd_quantize_mx8 of layernorm_kernel's bf16 output.  NV covers Kq columns.
+template <typename TI, int NV>
+__global__ __launch_bounds__(256) void layernorm_mx8_kernel(
+    const TI* __restrict__ x, int64_t rows, int D, int ldx, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, uint8_t* __restrict__ q, int ldq, int Kq,
+    uint8_t* __restrict__ sc, int64_t s_rows) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const TI* xr = x + row * ldx;
+  f32x4 v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    v[i] = c < D ? ld4(xr + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const float mean = s / D;
+  float qv = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if (c < D)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = v[i][j] - mean;
+        qv += d * d;
+      }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) qv += __shfl_xor(qv, o);
+  const float rstd = 1.f / sqrtf(qv / D + eps);
+  uint8_t* qr = q + row * ldq;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    f32x4 o = {0.f, 0.f, 0.f, 0.f};
+    if (c < D) {
+      const f32x4 g = *reinterpret_cast<const f32x4*>(gamma + c);
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(beta + c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = bf16_round((v[i][j] - mean) * rstd * g[j] + bb[j]);
+    }
+    float am = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3])));
+    am = fmaxf(am, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(am), 0xB1, 0xF, 0xF, false)));
+    am = fmaxf(am, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(am), 0x4E, 0xF, 0xF, false)));
+    am = fmaxf(am, __shfl_xor(am, 4));
+    const int E = mx8_exponent(am);
+    const float inv = __uint_as_float((uint32_t)(127 - E) << 23);
+    if (c < Kq) {
+      *reinterpret_cast<uint32_t*>(qr + c) = mx8_pack4(o[0], o[1], o[2], o[3], inv);
+      if ((lane & 7) == 0) {
+        const int b = c >> 5;
+        sc[((int64_t)(b >> 2) * s_rows + row) * 4 + (b & 3)] = (uint8_t)(E + 127);
+      }
+    }
+  }
+}
+
 // LayerNorm row statistics only (the fold path, vtd_epilogue.lnstat): one wave per RPW
 // rows (all their loads issued before the first reduction: the pass is a pure read
 // stream and needs the loads in flight), the same two-pass mean / variance as
@@ -429,6 +495,40 @@ int layernorm_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx, c
                            : ln_dispatch<float, float>(x, rows, D, ldx, g, b, eps, y, ldy, st);
 }
 
+int layernorm_mx8_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx,
+                         const float* g, const float* b, float eps, uint8_t* q, int ldq, int Kq,
+                         uint8_t* s, int64_t s_rows, hipStream_t st) {
+  VTD_CHECK_ARG(x && g && b && q && s, "layernorm_mx8: null pointer");
+  VTD_CHECK_ARG(rows > 0 && D > 0 && ldx >= D && Kq >= D && Kq % 128 == 0 && ldq >= Kq &&
+                    ldq % 16 == 0 && s_rows >= rows && Kq <= 4096,
+                "layernorm_mx8: bad shape (Kq % 128, D <= Kq <= 4096, ldq % 16, s_rows)");
+  VTD_CHECK_ARG(x_dtype == VTD_F32 || x_dtype == VTD_BF16, "layernorm_mx8: bad x dtype");
+  VTD_CHECK_ARG(D % 4 == 0 && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(g) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(b) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(x) % (x_dtype == VTD_BF16 ? 8 : 16) == 0,
+                "layernorm_mx8: D, ldx % 4 and 16-B aligned gamma / beta / x needed");
+  ProfScope ps(st, PROF_LN, 0.0);
+  const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  const int nv = (Kq + 255) / 256;
+#define VTD_LQ(TI, NV) hipLaunchKernelGGL((layernorm_mx8_kernel<TI, NV>), grid, block, 0, st,      \
+                                          static_cast<const TI*>(x), rows, D, ldx, g, b, eps, q, \
+                                          ldq, Kq, s, s_rows)
+  if (x_dtype == VTD_BF16) {
+    if (nv <= 2) VTD_LQ(bf16_t, 2);
+    else if (nv <= 4) VTD_LQ(bf16_t, 4);
+    else if (nv <= 8) VTD_LQ(bf16_t, 8);
+    else VTD_LQ(bf16_t, 16);
+  } else {
+    if (nv <= 2) VTD_LQ(float, 2);
+    else if (nv <= 4) VTD_LQ(float, 4);
+    else if (nv <= 8) VTD_LQ(float, 8);
+    else VTD_LQ(float, 16);
+  }
+#undef VTD_LQ
+  VTD_LAUNCH_CHECK("layernorm_mx8");
+  return VTD_OK;
+}
+
 int ln_stats_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx, float eps,
                     float* stat, hipStream_t st) {
   VTD_CHECK_ARG(x && stat, "layernorm_stats: null pointer");
@@ -523,6 +623,13 @@ int vtd_layernorm(const void* x_dev, int x_dtype, int64_t rows, int D, int ldx,
                   int dtype, void* stream) {
   return vtd::layernorm_launch(x_dev, x_dtype, rows, D, ldx, gamma_dev, beta_dev, eps, y_dev, ldy,
                                dtype, static_cast<hipStream_t>(stream));
+}
+
+int vtd_layernorm_mx8(const void* x_dev, int x_dtype, int64_t rows, int D, int ldx,
+                      const float* gamma_dev, const float* beta_dev, float eps, uint8_t* q_dev,
+                      int ldq, int Kq, uint8_t* s_dev, int64_t s_rows, void* stream) {
+  return vtd::layernorm_mx8_launch(x_dev, x_dtype, rows, D, ldx, gamma_dev, beta_dev, eps, q_dev,
+                                   ldq, Kq, s_dev, s_rows, static_cast<hipStream_t>(stream));
 }
 
 int vtd_layernorm_stats(const void* x_dev, int x_dtype, int64_t rows, int D, int ldx,

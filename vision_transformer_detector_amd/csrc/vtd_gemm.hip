@@ -39,6 +39,8 @@ struct EpiArgs {
   // partial LayerNorm statistics of the stored bf16 rows (fold path producer): per row m
   // and 64-column block b, statout[m * stat_ld + b] = (sum, sum of squares)
   float2* statout; int stat_ld;
+  // out_dtype VTD_FP8 (MX-fp8 GEMMs, fast epilogue): e4m3 out + E8M0 scales [n/128][s_rows][4]
+  uint8_t* sout; int64_t s_rows;
 };
 
 // v of another lane of the same 16-lane row by a DPP control (0 where the source is out
@@ -550,6 +552,32 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
       if constexpr (kDiagNoStore) {
         if (v0[0] != v0[0] && v1[3] != v1[3]) static_cast<float*>(e.out)[idx] = v0[1];
       } else if constexpr (OUT_BF16) {
+        if (e.out_dtype == VTD_FP8) {
+          // the next MX GEMM's operand: a 32-column block = 4 consecutive lanes (c8 / 8
+          // = 0..3 or 4..7), block amax by DPP quad xor 1 / xor 2; bf16-rounded values so
+          // the bytes equal vtd_quantize_mx8 of the bf16 output
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v0[j] = bf16_round(v0[j]);
+            v1[j] = bf16_round(v1[j]);
+          }
+          float am = 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) am = fmaxf(am, fmaxf(fabsf(v0[j]), fabsf(v1[j])));
+          am = fmaxf(am, dpp_f32<0xB1>(am));
+          am = fmaxf(am, dpp_f32<0x4E>(am));
+          const int E = mx8_exponent(am);
+          const float inv = __uint_as_float((uint32_t)(127 - E) << 23);
+          const uint2 qv = {mx8_pack4(v0[0], v0[1], v0[2], v0[3], inv),
+                            mx8_pack4(v1[0], v1[1], v1[2], v1[3], inv)};
+          *reinterpret_cast<uint2*>(static_cast<uint8_t*>(e.out) + idx) = qv;
+          if ((lane & 3) == 0) {
+            const int n = n_base + c8, b = n >> 5;
+            e.sout[((int64_t)(b >> 2) * e.s_rows + m_base + p * PR + row) * 4 + (b & 3)] =
+                (uint8_t)(E + 127);
+          }
+          continue;
+        }
         const i32x4 o = {(int)pack_bf16x2(v0[0], v0[1]), (int)pack_bf16x2(v0[2], v0[3]),
                          (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
         *reinterpret_cast<i32x4*>(static_cast<bf16_t*>(e.out) + idx) = o;
@@ -1661,6 +1689,15 @@ bool gemm_emits_stats(int M, int N, int dtype, const vtd_epilogue* e) {
          reinterpret_cast<uintptr_t>(e->statout) % 8 == 0;
 }
 
+// Whether vtd_gemm_mx8 can write its output as MX-fp8 (out_dtype VTD_FP8): the fast
+// epilogue on every tile, no residual or rare modes.
+bool gemm_mx8_emits_fp8(int M, int N, const vtd_epilogue* e) {
+  auto a16 = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
+  return M % BBM == 0 && N % BBN == 0 && e->bias && a16(e->bias) && !e->resid && !e->rowadd &&
+         !e->out2 && e->scatter_tokens <= 0 && !e->lnstat && e->ldo % 16 == 0 && a16(e->out) &&
+         e->scale_out && e->scale_rows >= M && e->scale_rows % 4 == 0;
+}
+
 int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
                 int dtype, const vtd_epilogue* epi, hipStream_t stream, double flops) {
   VTD_CHECK_ARG(M > 0 && N > 0 && K > 0, "gemm: M, N, K must be positive");
@@ -1684,7 +1721,8 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
             epi->rowadd ? epi->rowadd_ncols : 0, epi->act, epi->resid, epi->ldr,
             epi->out, epi->ldo, epi->out_dtype, epi->out2, epi->ldo2,
             epi->scatter_tokens, reinterpret_cast<const float2*>(epi->lnstat), epi->colsum,
-            reinterpret_cast<float2*>(epi->statout), epi->stat_ld};
+            reinterpret_cast<float2*>(epi->statout), epi->stat_ld, epi->scale_out,
+            epi->scale_rows};
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM);
   const size_t lds = 4 * TILE_BYTES;
   ProfScope ps(stream, PROF_GEMM, flops > 0 ? flops : 2.0 * M * N * (double)K);
@@ -1843,7 +1881,8 @@ int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_
                 "gemm_mx8: lda/ldb must be >= K and multiples of 16");
   VTD_CHECK_ARG(sa_rows >= M && sb_rows >= N && sa_rows % 4 == 0 && sb_rows % 4 == 0,
                 "gemm_mx8: scale row counts must cover M / N and be multiples of 4");
-  VTD_CHECK_ARG(epi->out_dtype == VTD_F32 || epi->out_dtype == VTD_BF16, "gemm_mx8: bad out dtype");
+  VTD_CHECK_ARG(epi->out_dtype == VTD_F32 || epi->out_dtype == VTD_BF16 ||
+                    epi->out_dtype == VTD_FP8, "gemm_mx8: bad out dtype");
   VTD_CHECK_ARG(!epi->rowadd || epi->rowadd_period > 0, "gemm_mx8: rowadd_period");
   VTD_CHECK_ARG(epi->scatter_tokens <= 0 || N <= VTD_MAX_DETECT,
                 "gemm_mx8: scatter epilogue needs N <= 17");
@@ -1851,11 +1890,16 @@ int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_
                                  reinterpret_cast<uintptr_t>(epi->colsum) % 16 == 0),
                 "gemm_mx8: lnstat needs colsum (16-B aligned) and 8-B alignment");
   if (epi->statout) return fail(VTD_ERR_UNSUPPORTED, "gemm_mx8: statout is not supported");
+  if (epi->out_dtype == VTD_FP8 && !gemm_mx8_emits_fp8(M, N, epi))
+    return fail(VTD_ERR_UNSUPPORTED, "gemm_mx8: an MX-fp8 output needs full 256 x 256 tiles, a "
+                                     "bias, no residual / rowadd / out2 / scatter, ldo % 16 and "
+                                     "scale_rows >= M, % 4");
   EpiArgs e{epi->bias, epi->rowadd, epi->rowadd_period,
             epi->rowadd ? epi->rowadd_ncols : 0, epi->act, epi->resid, epi->ldr,
             epi->out, epi->ldo, epi->out_dtype, epi->out2, epi->ldo2,
             epi->scatter_tokens, reinterpret_cast<const float2*>(epi->lnstat), epi->colsum,
-            reinterpret_cast<float2*>(epi->statout), epi->stat_ld};
+            reinterpret_cast<float2*>(epi->statout), epi->stat_ld, epi->scale_out,
+            epi->scale_rows};
   ProfScope ps(stream, PROF_GEMM, flops > 0 ? flops : 2.0 * M * N * (double)K);
   const int tiles_m = (M + BBM - 1) / BBM, tiles_n = (N + BBN - 1) / BBN;
   static bool attr = false;
@@ -1874,7 +1918,7 @@ int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_
                     reinterpret_cast<uintptr_t>(e.out) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(e.bias) % 16 == 0 &&
                     (!e.resid || reinterpret_cast<uintptr_t>(e.resid) % 16 == 0);
-  const int code = fast ? epi_code(e.act, e.out_dtype == VTD_BF16, e.resid != nullptr)
+  const int code = fast ? epi_code(e.act, e.out_dtype != VTD_F32, e.resid != nullptr)
                         : EPI_GENERIC;
   const dim3 g(tiles_m * tiles_n), b(BNT);
   switch (code) {

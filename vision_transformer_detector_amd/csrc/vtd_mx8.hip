@@ -17,14 +17,6 @@ namespace vtd {
 
 namespace {
 
-__device__ __forceinline__ int mx8_exponent(float amax) {
-  const uint32_t b = __float_as_uint(amax);
-  const int e = (int)((b >> 23) & 0xff);
-  if (e == 0) return -126;                           // zero / subnormal block
-  const int E = e - 126 - 9 + ((b & 0x7fffff) > 0x600000 ? 1 : 0);
-  return min(max(E, -126), 126);
-}
-
 // one thread per 32-element block; consecutive threads take consecutive blocks of a row
 template <typename T>
 __global__ __launch_bounds__(256) void quantize_mx8_kernel(

@@ -27,6 +27,10 @@ int patches_launch(const float* img, int B, int H, int W, int C, int p, void* ou
 int decode_launch(const float* logits, int64_t n, float* dets, hipStream_t st);
 int quantize_mx8_launch(const void* x, int x_dtype, int64_t rows, int K, int ldx, int Kq,
                         uint8_t* q, int ldq, uint8_t* s, int64_t s_rows, hipStream_t st);
+int layernorm_mx8_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx,
+                         const float* g, const float* b, float eps, uint8_t* q, int ldq, int Kq,
+                         uint8_t* s, int64_t s_rows, hipStream_t st);
+bool gemm_mx8_emits_fp8(int M, int N, const vtd_epilogue* e);
 int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_t* sA,
                     int64_t sa_rows, const uint8_t* Bt, int ldb, const uint8_t* sB,
                     int64_t sb_rows, const vtd_epilogue* epi, hipStream_t stream,
@@ -142,7 +146,8 @@ static int derive(const vtd_config* c, vtd_dims* d) {
 
 namespace {
 struct Plan {
-  size_t patches, x, xb, h, stat, pstat, qkv, attn, mlp0, mlp1, u, head0, head1, q8, s8, total;
+  size_t patches, x, xb, h, stat, pstat, qkv, attn, mlp0, mlp1, u, head0, head1, q8, s8, q8b, s8b,
+      total;
   int k8_max;                       // widest MX-fp8 GEMM K (VTD_FP8)
   int64_t s8_rows;                  // activation scale rows (rows rounded up to 4)
 };
@@ -193,8 +198,11 @@ Plan make_plan(const vtd_config* c, const vtd_dims& d) {
     p.k8_max = std::max(k8_of(d.d_p), k8_of(d.inner_p));
     for (int j = 0; j + 1 < c->mlp_quantities; ++j) p.k8_max = std::max(p.k8_max, k8_of(d.mlp_units_p[j]));
   }
+  // two MX-fp8 operand buffers: an MLP GEMM reads one and writes the next one's operand
   p.q8 = take(R * p.k8_max);
   p.s8 = take((size_t)p.s8_rows * p.k8_max / 32);
+  p.q8b = take(R * p.k8_max);
+  p.s8b = take((size_t)p.s8_rows * p.k8_max / 32);
   p.total = off;
   return p;
 }
@@ -393,6 +401,20 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     return gemm_mx8_launch(M, Np, K8, q8, K8, s8, P.s8_rows, static_cast<const uint8_t*>(W), K8,
                            S, Np, e, st, flops);
   };
+  // VTD_FP8: the GEMM on an operand a producer already wrote as MX-fp8 (q, s)
+  uint8_t* q8b = reinterpret_cast<uint8_t*>(ws + P.q8b);
+  uint8_t* s8b = reinterpret_cast<uint8_t*>(ws + P.s8b);
+  auto mx_gemm = [&](int Np, int K, const uint8_t* qa, const uint8_t* sa, const void* W,
+                     const uint8_t* S, const vtd_epilogue* e, double flops) -> int {
+    const int K8 = k8_of(K);
+    return gemm_mx8_launch(M, Np, K8, qa, K8, sa, P.s8_rows, static_cast<const uint8_t*>(W), K8,
+                           S, Np, e, st, flops);
+  };
+  // VTD_FP8 LayerNorm straight into the MX-fp8 operand buffer q8 / s8
+  auto ln_mx8 = [&](const float* g, const float* b) -> int {
+    return layernorm_mx8_launch(x, rdt, R, D, Dp, g, b, 1e-3f, q8, k8_of(Dp), k8_of(Dp), s8,
+                                P.s8_rows, st);
+  };
 
   // ---- ExtractImagePatches + flatten (vtd.py:271-280)
   rc = patches_launch(images, B, cfg->image_h, cfg->image_w, cfg->channels,
@@ -421,6 +443,8 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     if (L.ln1_colsum) {
       rc = row_stats();
       a1 = x;
+    } else if (fp8) {
+      rc = ln_mx8(L.ln1_gamma, L.ln1_beta);       // LayerNorm + MX quantization, one pass
     } else {
       rc = layernorm_launch(x, rdt, R, D, Dp, L.ln1_gamma, L.ln1_beta, 1e-3f, h, Dp, dt, st);
     }
@@ -430,8 +454,9 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
       e.bias = L.b_qkv; e.act = VTD_ACT_NONE;
       e.out = qkv; e.ldo = d.qkv_p; e.out_dtype = dt;
       if (L.ln1_colsum) { e.lnstat = stat; e.colsum = L.ln1_colsum; }
-      rc = enc_gemm(d.qkv_p, Dp, a1, L.w_qkv, L.s_qkv, &e,
-                    2.0 * fR * D * 3.0 * cfg->num_heads * cfg->key_dim);
+      const double fl = 2.0 * fR * D * 3.0 * cfg->num_heads * cfg->key_dim;
+      rc = fp8 ? mx_gemm(d.qkv_p, Dp, q8, s8, L.w_qkv, L.s_qkv, &e, fl)
+               : enc_gemm(d.qkv_p, Dp, a1, L.w_qkv, L.s_qkv, &e, fl);
       if (rc) return rc;
     }
     rc = attention_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale, attn,
@@ -449,9 +474,15 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
       if (rc) return rc;
     }
     const void* a = h;
+    // VTD_FP8: the current MLP operand as MX-fp8 (aq, as), written by its producer
+    const uint8_t* aq = nullptr;
+    const uint8_t* as = nullptr;
     if (L.ln2_colsum) {
       rc = row_stats();
       a = x;
+    } else if (fp8) {
+      rc = ln_mx8(L.ln2_gamma, L.ln2_beta);
+      aq = q8; as = s8;
     } else {
       rc = layernorm_launch(x, rdt, R, D, Dp, L.ln2_gamma, L.ln2_beta, 1e-3f, h, Dp, dt, st);
     }
@@ -472,10 +503,26 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
       } else {
         e.out = mlp[j & 1]; e.ldo = d.mlp_units_p[j]; e.out_dtype = dt;
       }
-      rc = enc_gemm(d.mlp_units_p[j], k, a, L.w_mlp[j], L.s_mlp[j], &e,
-                    2.0 * fR * kv * d.mlp_units[j]);
+      // VTD_FP8: an inner MLP layer writes the next layer's MX-fp8 operand itself (into the
+      // operand buffer it is not reading) when every tile takes the fast epilogue
+      uint8_t* nq = nullptr;
+      uint8_t* ns = nullptr;
+      if (fp8 && !last) {
+        nq = aq == q8b ? q8 : q8b;        // (enc_gemm quantizes into q8)
+        ns = aq == q8b ? s8 : s8b;
+        vtd_epilogue ef = e;
+        ef.out = nq; ef.ldo = k8_of(d.mlp_units_p[j]); ef.out_dtype = VTD_FP8;
+        ef.scale_out = ns; ef.scale_rows = P.s8_rows;
+        if (gemm_mx8_emits_fp8(M, d.mlp_units_p[j], &ef)) e = ef;
+        else nq = ns = nullptr;
+      }
+      const double fl = 2.0 * fR * kv * d.mlp_units[j];
+      rc = aq ? mx_gemm(d.mlp_units_p[j], k, aq, as, L.w_mlp[j], L.s_mlp[j], &e, fl)
+              : enc_gemm(d.mlp_units_p[j], k, a, L.w_mlp[j], L.s_mlp[j], &e, fl);
       if (rc) return rc;
       a = mlp[j & 1];
+      aq = nq;
+      as = ns;
       k = d.mlp_units_p[j];
       kv = d.mlp_units[j];
     }
