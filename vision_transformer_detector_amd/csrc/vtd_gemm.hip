@@ -1656,6 +1656,198 @@ __global__ __launch_bounds__(BNT) void gemm_mx8_kernel(
   }
   epilogue_generic(acc, ep, lane, M, N, m_base, n_base, e);
 }
+
+// ---------------------------------------------------------------------------------
+// Ping-pong MX-fp8 GEMM ("mxp"): pp2's K loop (four 16-KiB DMA groups per stage, the
+// two wave groups offset by one barrier, counted vmcnt) on MX-fp8 operands.  A K-step of
+// 128 fp8 elements is 128 B per row, the same LDS image as a bf16 K-step of 64: the DMA,
+// the swizzle and the fragment reads are pp2's byte for byte, and a bf16 pair of
+// fragments (chunks fg and fg + 4 of a row) IS the MX operand of
+// v_mfma_scale_f32_16x16x128_f8f6f4 (lane group fg supplies K [16 fg, +16) and
+// [64 + 16 fg, +16): tools/mx8_probe.py).  One MX MFMA replaces the two bf16 k-substeps at
+// the same cycles, so a phase is 8 MFMAs of 32 cycles.
+// Scales: per stage, 1 KiB of A scales (256 rows x 4 block bytes) rides with group X0 and
+// 1 KiB of B scales with Y0 (lanes 0-7 of every wave, 128 B each: 3 DMA instructions in
+// those groups, 2 in X1 / Y1); a wave reads all 8 A and 4 B scale dwords of the tile in
+// P0, so X0(t+2) / Y0(t+2) overwrite them under the same WAR argument as their operands.
+// Waits (youngest first, per tile: X1 2, X0 3, Y0 3, Y1 2): P0 vmcnt(12) -> Y0, Y1(t);
+// P1 vmcnt(10) -> X1(t); P3 vmcnt(12) -> X0, Y0(t+1).
+constexpr int MXP_STAGE = BSTAGE + 2048;      // 66 KiB
+
+struct MxpSrc {
+  __amdgpu_buffer_rsrc_t ra, rb, rsa, rsb;
+  int off[4][2];
+  int vsa, vsb, sa4, sb4;                    // scale voffsets, scale K-step strides (bytes)
+};
+
+template <int G>
+__device__ __forceinline__ void mxp_issue(char* smem, const MxpSrc& src, int wave, int lane,
+                                          int kt, int stage) {
+  char* st = smem + stage * MXP_STAGE;
+  char* dst = st + G * 16384 + wave * 2 * 1024;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(G < 2 ? src.ra : src.rb,
+                                             (lds_void_t*)(dst + j * 1024), 16, src.off[G][j],
+                                             kt * 128, 0, 0);
+  if constexpr (G == 0 || G == 2) {
+    if (lane < 8)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          G == 0 ? src.rsa : src.rsb, (lds_void_t*)(st + BSTAGE + (G == 0 ? 0 : 1024) + wave * 128),
+          16, G == 0 ? src.vsa : src.vsb, kt * (G == 0 ? src.sa4 : src.sb4), 0, 0);
+  }
+}
+
+typedef __attribute__((ext_vector_type(8))) int i32x8_t;
+__device__ __forceinline__ i32x8_t mx_operand(const bf16x8& lo, const bf16x8& hi) {
+  return __builtin_shufflevector(__builtin_bit_cast(i32x4, lo), __builtin_bit_cast(i32x4, hi), 0,
+                                 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <int I0, int J0>
+__device__ __forceinline__ void mxp_mfma(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][2],
+                                         const bf16x8 (&b)[2][2], const int (&sa)[8],
+                                         const int (&sb)[4]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      acc[I0 + i][J0 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+          mx_operand(a[i][0], a[i][1]), mx_operand(b[j][0], b[j][1]), acc[I0 + i][J0 + j], 0, 0,
+          0, sa[I0 + i], 0, sb[J0 + j]);
+  // pin the cluster inside its phase: without these the compiler sinks every scaled MFMA
+  // of the K-step past the phase barriers to the end of the loop body (no ping-pong left)
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(acc[I0 + i][J0 + j]));
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(BNT) void gemm_mx8_pp_kernel(
+    int M, int N, int K, const uint8_t* __restrict__ A, int lda, const uint8_t* __restrict__ sA,
+    int64_t sa_rows, const uint8_t* __restrict__ Bt, int ldb, const uint8_t* __restrict__ sB,
+    int64_t sb_rows, int tiles_m, int tiles_n, EpiArgs e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tm = tile / tiles_n, tn = tile - (tile / tiles_n) * tiles_n;
+  const int m0 = tm * BBM, n0 = tn * BBN;
+  MxpSrc src;
+  {
+    const int64_t ra_bytes = (int64_t)(M - m0) * lda, rb_bytes = (int64_t)(N - n0) * ldb;
+    src.ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(A + (int64_t)m0 * lda), 0,
+                                               (int)std::min<int64_t>(ra_bytes, 0x7fffffff), 0x00020000);
+    src.rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(Bt + (int64_t)n0 * ldb), 0,
+                                               (int)std::min<int64_t>(rb_bytes, 0x7fffffff), 0x00020000);
+    src.rsa = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sA), 0,
+                                                (int)std::min<int64_t>(sa_rows * K / 32, 0x7fffffff), 0x00020000);
+    src.rsb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sB), 0,
+                                                (int)std::min<int64_t>(sb_rows * K / 32, 0x7fffffff), 0x00020000);
+    const int prow = lane >> 3, pchunk = (lane & 7) ^ prow;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int tr = grp_tile_row(g, (wave * 2 + j) * 8 + prow);
+        src.off[g][j] = g < 2 ? min(tr, M - 1 - m0) * lda + pchunk * 16
+                              : min(tr, N - 1 - n0) * ldb + pchunk * 16;
+      }
+    // scales: lanes 0-7 of wave w copy the dwords of tile rows 32 w + 4 l .. + 3 (rows past
+    // the end read beyond sa_rows / sb_rows fall outside the records: zero)
+    src.vsa = (m0 + wave * 32 + 4 * (lane & 7)) * 4;
+    src.vsb = (n0 + wave * 32 + 4 * (lane & 7)) * 4;
+    src.sa4 = (int)(sa_rows * 4);
+    src.sb4 = (int)(sb_rows * 4);
+  }
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fg = lane >> 4;
+  const int nk = K / 128;
+  // prologue: tile 0 complete, tile 1's X0 / Y0 / Y1 in flight
+  mxp_issue<0>(smem, src, wave, lane, 0, 0);
+  mxp_issue<2>(smem, src, wave, lane, 0, 0);
+  mxp_issue<3>(smem, src, wave, lane, 0, 0);
+  mxp_issue<1>(smem, src, wave, lane, 0, 0);
+  if (nk > 1) {
+    mxp_issue<0>(smem, src, wave, lane, 1, 1);
+    mxp_issue<2>(smem, src, wave, lane, 1, 1);
+    mxp_issue<3>(smem, src, wave, lane, 1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  pp_barrier();
+  if (wm == 1) pp_barrier();                 // stagger G1 by one barrier
+  const int ra = wm * 64, rb = wn * 32;      // group rows of this wave's quads
+  const int sa_row = wm * 128 + fr, sb_row = wn * 64 + fr;
+  bf16x8 a[4][2], b0[2][2], b1[2][2];
+  int sa[8], sb[4];
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* st = smem + (kt & 1) * MXP_STAGE;
+    const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+    // ---- P0 (also every scale of the tile: X0 / Y0 refill them two tiles ahead)
+    pp_load_a(a, st + 0 * 16384, ra, fr, fg);
+    pp_load_b(b0, st + 2 * 16384, rb, fr, fg);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      sa[i] = *reinterpret_cast<const int*>(st + BSTAGE + (sa_row + 16 * i) * 4) >> (8 * fg);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      sb[j] = *reinterpret_cast<const int*>(st + BSTAGE + 1024 + (sb_row + 16 * j) * 4) >> (8 * fg);
+    if (n1) mxp_issue<1>(smem, src, wave, lane, kt + 1, (kt + 1) & 1);
+    if (n1) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pp_barrier();
+    mxp_mfma<0, 0>(acc, a, b0, sa, sb);
+    pp_barrier();
+    // ---- P1
+    pp_load_b(b1, st + 3 * 16384, rb, fr, fg);
+    if (n1) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pp_barrier();
+    mxp_mfma<0, 2>(acc, a, b1, sa, sb);
+    pp_barrier();
+    // ---- P2
+    pp_load_a(a, st + 1 * 16384, ra, fr, fg);
+    if (n2) mxp_issue<0>(smem, src, wave, lane, kt + 2, kt & 1);
+    pp_barrier();
+    mxp_mfma<4, 2>(acc, a, b1, sa, sb);
+    pp_barrier();
+    // ---- P3
+    if (n2) {
+      mxp_issue<2>(smem, src, wave, lane, kt + 2, kt & 1);
+      mxp_issue<3>(smem, src, wave, lane, kt + 2, kt & 1);
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    pp_barrier();
+    mxp_mfma<4, 0>(acc, a, b0, sa, sb);
+    pp_barrier();
+  }
+  if (wm == 0) pp_barrier();                 // re-align
+  float* ep = reinterpret_cast<float*>(smem) + wave * 32 * 68;
+  const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
+  if constexpr (EPI != EPI_GENERIC) {
+    if (m0 + BBM <= M && n0 + BBN <= N) {
+      epilogue_fast<EPI>(acc, ep, lane, m_base, n_base, e);
+      return;
+    }
+  }
+  epilogue_generic(acc, ep, lane, M, N, m_base, n_base, e);
+}
 }  // namespace
 
 bool gemm_pp3_launch(int M, int N, int K, const bf16_t* A, int lda, const bf16_t* Bt,
@@ -1904,13 +2096,15 @@ int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_
   const int tiles_m = (M + BBM - 1) / BBM, tiles_n = (N + BBN - 1) / BBN;
   static bool attr = false;
   if (!attr) {
-#define VTD_MX_FN(C) reinterpret_cast<const void*>(&gemm_mx8_kernel<C>),
+#define VTD_MX_FN(C) reinterpret_cast<const void*>(&gemm_mx8_kernel<C>), \
+                     reinterpret_cast<const void*>(&gemm_mx8_pp_kernel<C>),
     const void* fns[] = {VTD_MX_FN(EPI_GENERIC) VTD_MX_FN(0) VTD_MX_FN(1) VTD_MX_FN(2)
                          VTD_MX_FN(4) VTD_MX_FN(5) VTD_MX_FN(6) VTD_MX_FN(8) VTD_MX_FN(9)
                          VTD_MX_FN(10) VTD_MX_FN(12) VTD_MX_FN(13) VTD_MX_FN(14)};
 #undef VTD_MX_FN
     for (const void* f : fns)
-      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * MX_STAGE);
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                std::max(2 * MX_STAGE, 2 * MXP_STAGE));
     attr = true;
   }
   const bool fast = e.bias && !e.rowadd && e.scatter_tokens <= 0 && !e.out2 &&
@@ -1921,19 +2115,32 @@ int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_
   const int code = fast ? epi_code(e.act, e.out_dtype != VTD_F32, e.resid != nullptr)
                         : EPI_GENERIC;
   const dim3 g(tiles_m * tiles_n), b(BNT);
+  // 1 (default): ping-pong MX kernel; 0: the two-barrier MX kernel
+  static const int mxv = [] {
+    const char* v = getenv("VTD_MX_VARIANT");
+    return v ? atoi(v) : 1;
+  }();
   switch (code) {
 #define VTD_MX_CASE(C)                                                                     \
   case C:                                                                                  \
-    hipLaunchKernelGGL((gemm_mx8_kernel<C>), g, b, 2 * MX_STAGE, stream, M, N, K, A, lda,  \
-                       sA, sa_rows, Bt, ldb, sB, sb_rows, tiles_m, tiles_n, e);            \
+    if (mxv == 1)                                                                          \
+      hipLaunchKernelGGL((gemm_mx8_pp_kernel<C>), g, b, 2 * MXP_STAGE, stream, M, N, K, A, \
+                         lda, sA, sa_rows, Bt, ldb, sB, sb_rows, tiles_m, tiles_n, e);     \
+    else                                                                                   \
+      hipLaunchKernelGGL((gemm_mx8_kernel<C>), g, b, 2 * MX_STAGE, stream, M, N, K, A, lda,\
+                         sA, sa_rows, Bt, ldb, sB, sb_rows, tiles_m, tiles_n, e);          \
     break;
     VTD_MX_CASE(0) VTD_MX_CASE(1) VTD_MX_CASE(2) VTD_MX_CASE(4) VTD_MX_CASE(5)
     VTD_MX_CASE(6) VTD_MX_CASE(8) VTD_MX_CASE(9) VTD_MX_CASE(10) VTD_MX_CASE(12)
     VTD_MX_CASE(13) VTD_MX_CASE(14)
 #undef VTD_MX_CASE
     default:
-      hipLaunchKernelGGL((gemm_mx8_kernel<EPI_GENERIC>), g, b, 2 * MX_STAGE, stream, M, N, K,
-                         A, lda, sA, sa_rows, Bt, ldb, sB, sb_rows, tiles_m, tiles_n, e);
+      if (mxv == 1)
+        hipLaunchKernelGGL((gemm_mx8_pp_kernel<EPI_GENERIC>), g, b, 2 * MXP_STAGE, stream, M, N,
+                           K, A, lda, sA, sa_rows, Bt, ldb, sB, sb_rows, tiles_m, tiles_n, e);
+      else
+        hipLaunchKernelGGL((gemm_mx8_kernel<EPI_GENERIC>), g, b, 2 * MX_STAGE, stream, M, N, K,
+                           A, lda, sA, sa_rows, Bt, ldb, sB, sb_rows, tiles_m, tiles_n, e);
   }
   VTD_LAUNCH_CHECK("gemm_mx8");
   return VTD_OK;
