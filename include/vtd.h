@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define VTD_ABI_VERSION 6
+#define VTD_ABI_VERSION 7
 #define VTD_KALIGN 64          /* K / row padding granule, elements              */
 #define VTD_MAX_MLP 16         /* max encoder_mlp_quantities                     */
 #define VTD_MAX_HEAD 64        /* max mlp_head layers * repeats                   */
@@ -258,6 +258,21 @@ int vtd_decode(const float* logits_dev, int64_t n, float* dets_dev, void* stream
 int vtd_decode_detections(const float* logits_dev, int64_t n, float* dets_dev,
                           int32_t* category_dev, uint8_t* valid_dev, float obj_threshold,
                           float cls_threshold, void* stream);
+
+/* ---------------------------------------------------------------- input ------- */
+/* _get_image_tensor_coco after decode (vision_transformer_utilities.py:418-449):
+ * tf.image.resize_with_pad(image, target_h, target_w) (bilinear, half-pixel centers, no
+ * antialias; TF 2.9 float32 geometry: ratio = max(w/tw, h/th), resized = floor(side/ratio),
+ * pad_before = floor((target - side/ratio)/2)) -> clip [0, 255] -> /127.5 -> -1.
+ * pixels_dev: B decoded uint8 HWC (C = 3) images, image b at byte offset offsets_dev[b];
+ * sizes_dev: int32 [B][2] = (height, width). out_dev: fp32 NHWC [B][target_h][target_w][3]
+ * in [-1, 1] (pad = -1), i.e. the `images` argument of vtd_forward. Images whose resized
+ * side would be 0 (TF raises for them) must be rejected by the caller: the kernel writes
+ * the pad value for them. Replaces the tf.image / tf.clip_by_value / arithmetic ops at
+ * vision_transformer_utilities.py:438-447. */
+int vtd_resize_with_pad(const uint8_t* pixels_dev, const int64_t* offsets_dev,
+                        const int32_t* sizes_dev, int B, int target_h, int target_w,
+                        float* out_dev, void* stream);
 
 /* ---------------------------------------------------------------- forward ------ */
 /* model(images, training=False) (vtd.py:579-581, ipynb:836):

@@ -11,7 +11,8 @@ from .detector import (Constants, Model, create_vision_transformer_detector,  # 
                        keras_weight_names, transform_predictions)
 from .metrics import MeanAveragePrecision, iou_calculator  # noqa: F401
 from . import presets  # noqa: F401
+from .preprocess import get_image_tensors  # noqa: F401
 
 __all__ = ["Constants", "Model", "create_vision_transformer_detector",
            "transform_predictions", "decode_detections", "detection_list", "presets",
-           "MeanAveragePrecision", "iou_calculator"]
+           "MeanAveragePrecision", "iou_calculator", "get_image_tensors"]

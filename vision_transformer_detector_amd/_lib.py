@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede loading libvtd.so, see module doc)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvtd.so")
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 KALIGN = 64
 MAX_MLP = 16
 MAX_HEAD = 64
@@ -109,6 +109,8 @@ SIGNATURES = {
     "vtd_decode": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "vtd_decode_detections": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                       c_float, c_float, c_void_p]),
+    "vtd_resize_with_pad": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                                    c_void_p]),
     "vtd_iou": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
     "vtd_map_reset": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "vtd_map_update": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,

@@ -1,0 +1,63 @@
+"""Input pipeline image transform on the device.
+
+Mirrors `_get_image_tensor_coco` (`vision_transformer_utilities.py:418-449`) for a batch of
+already decoded images: `tf.image.resize_with_pad` to the model size (bilinear, half-pixel
+centers), `clip_by_value(0, 255)`, `/ 127.5 - 1`, written as one NHWC fp32 batch that
+`Model.__call__` takes directly. One `vtd_resize_with_pad` launch per batch; file reading and
+JPEG/PNG decode (`tf.io.read_file` / `tf.image.decode_image`) stay with the caller.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+MODEL_IMAGE_HEIGHT, MODEL_IMAGE_WIDTH = 608, 608   # vtd.py:22 Constants.MODEL_IMAGE_SIZE
+
+
+def _resized_side_positive(h: int, w: int, th: int, tw: int) -> bool:
+    # TF's float32 geometry (image_ops_impl._resize_image_with_pad_common): a side that
+    # floors to 0 makes ResizeBilinear raise; reject it here the same way.
+    f = np.float32
+    ratio = max(f(w) / f(tw), f(h) / f(th))
+    return np.floor(f(h) / ratio) >= 1 and np.floor(f(w) / ratio) >= 1
+
+
+def get_image_tensors(images, target_height: int = MODEL_IMAGE_HEIGHT,
+                      target_width: int = MODEL_IMAGE_WIDTH, device="cuda", stream=None):
+    """Decoded uint8 HWC images (numpy arrays or torch tensors, any sizes, 3 channels) ->
+    (images (B, target_height, target_width, 3) fp32 in [-1, 1] on `device`,
+     original sizes [(height, width), ...]) — the batched form of the reference's
+    `image_tensor, image_original_size = _get_image_tensor_coco(path)`."""
+    if len(images) == 0:
+        raise ValueError("get_image_tensors: empty image list")
+    if target_height <= 0 or target_width <= 0:
+        raise ValueError("get_image_tensors: target size must be positive")
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise ValueError(f"get_image_tensors runs on a HIP device, got {dev}")
+    sizes, flats = [], []
+    for img in images:
+        t = torch.as_tensor(img)
+        if t.dtype != torch.uint8 or t.dim() != 3 or t.shape[2] != 3:
+            raise ValueError(f"expected a uint8 (H, W, 3) image, got {tuple(t.shape)} {t.dtype}")
+        h, w = int(t.shape[0]), int(t.shape[1])
+        if h <= 0 or w <= 0 or not _resized_side_positive(h, w, target_height, target_width):
+            raise ValueError(f"image {h}x{w} cannot be resized with pad to "
+                             f"{target_height}x{target_width} (a resized side would be 0)")
+        sizes.append((h, w))
+        flats.append(t.reshape(-1))
+    lengths = [int(f.numel()) for f in flats]
+    offsets = np.zeros(len(flats), np.int64)
+    offsets[1:] = np.cumsum(lengths[:-1])
+    packed = torch.cat([f.cpu() for f in flats]).pin_memory()
+    pixels = packed.to(dev, non_blocking=True)
+    offs = torch.from_numpy(offsets).to(dev)
+    szs = torch.tensor(sizes, dtype=torch.int32).to(dev)
+    out = torch.empty(len(flats), target_height, target_width, 3, dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        L.check(L.lib.vtd_resize_with_pad(L.ptr(pixels), L.ptr(offs), L.ptr(szs), len(flats),
+                                          target_height, target_width, L.ptr(out),
+                                          L.stream_ptr(stream)), "resize_with_pad")
+    return out, sizes
