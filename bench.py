@@ -135,6 +135,9 @@ def main():
     ap.add_argument("--streams", type=int, default=2,
                     help="vtd_forward micro-batch streams (VTD_STREAMS; 1 = one stream)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--graph", type=int, default=0,
+                    help="1: the forward of a step is one HIP-graph replay (captured once after "
+                         "warm-up); 0: eager vtd_forward calls")
     args = ap.parse_args()
     os.environ["VTD_STREAMS"] = str(args.streams)      # read once by libvtd.so
 
@@ -161,15 +164,39 @@ def main():
 
     from vision_transformer_detector_amd.distributed import all_gather_detections
 
-    def step():
+    def eager_step():
         logits, dets = model.detect(images)
         if world > 1:                        # the path's one exchange: RCCL all-gather
             all_gather_detections(dets, world * B)
         return logits
 
+    step = eager_step
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    if args.graph:
+        # the whole forward (every kernel of vtd_forward, both micro-batch streams, the
+        # decode) captured once as a HIP graph on a side stream and replayed per step: the
+        # same launches without per-launch host work or inter-kernel gaps.  The RCCL
+        # all-gather stays outside the graph.
+        cs = torch.cuda.Stream(device=dev)
+        cs.wait_stream(torch.cuda.current_stream())
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(cs):
+            model.detect(images)             # workspace / internal stream exist before capture
+            with torch.cuda.graph(graph, stream=cs):
+                g_logits, g_dets = model.detect(images)
+        torch.cuda.current_stream().wait_stream(cs)
+        torch.cuda.synchronize()
+
+        def step():
+            graph.replay()
+            if world > 1:
+                all_gather_detections(g_dets, world * B)
+            return g_logits
+
+        step()
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -195,7 +222,7 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        eager_step()                         # profiling hooks run at launch time: eager
     torch.cuda.synchronize()
     prof_elapsed = time.perf_counter() - t1
     L.check(L.lib.vtd_profile_enable(0))
@@ -233,7 +260,8 @@ def main():
         "config": {"workload": f"{args.preset} detector forward + decode + all-gather of "
                                f"detections", "per_gpu_batch": B, "global_batch": world * B,
                    "input_shape": list(shape), "tokens": model.dims.tokens,
-                   "parallelism": f"dp{world}", "streams_per_gpu": args.streams},
+                   "parallelism": f"dp{world}", "streams_per_gpu": args.streams,
+                   "hip_graph": bool(args.graph)},
         "mfma_util_attn_mlp": round(attn_mlp_fl * img_s / world / (peak * 1e12), 4),
         "model_tflops_per_gpu": round(total_fl * img_s / world / 1e12, 1),
         "roofline": {"bound": "mfma",
