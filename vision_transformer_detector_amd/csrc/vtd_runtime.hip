@@ -212,14 +212,17 @@ Plan make_plan(const vtd_config* c, const vtd_dims& d) {
 // tiles of an N = 768 layer = 2.3 rounds of 256 CUs) runs beside the other half's work
 // instead of leaving CUs idle.  VTD_STREAMS=1 disables it; so does per-kernel profiling
 // (vtd_profile_enable): each profiled launch then runs alone and its events time it.
+constexpr int kMaxSplit = 4;   // VTD_STREAMS is clamped to [1, kMaxSplit]
 int split_count(const vtd_config* c, const vtd_dims& d) {
   if (prof().enabled) return 1;
   static const int streams = [] {
     const char* v = getenv("VTD_STREAMS");
     return v ? atoi(v) : 2;
   }();
-  // only where each half still has >= 48 row tiles of 256 (C2 at B = 256: 98 each)
-  return streams >= 2 && c->batch >= 2 && d.rows >= (int64_t)2 * 48 * 256 ? 2 : 1;
+  // only where each part still has >= 48 row tiles of 256 (C2 at B = 256, 2 parts: 98 each)
+  int ns = std::min(std::max(streams, 1), (int)kMaxSplit);
+  while (ns > 1 && (c->batch < ns || d.rows < (int64_t)ns * 48 * 256)) --ns;
+  return ns;
 }
 vtd_config sub_config(const vtd_config* c, int part, int nsplit) {
   vtd_config s = *c;
@@ -234,7 +237,10 @@ size_t split_workspace(const vtd_config* c, const vtd_dims& d) {
     const char* v = getenv("VTD_STREAMS");
     return v ? atoi(v) : 2;
   }();
-  const int ns = streams >= 2 && c->batch >= 2 ? 2 : 1;
+  vtd_dims dd;
+  if (derive(c, &dd) != VTD_OK) return 0;
+  int ns = std::min(std::max(streams, 1), (int)kMaxSplit);
+  while (ns > 1 && (c->batch < ns || dd.rows < (int64_t)ns * 48 * 256)) --ns;
   if (ns == 1) return whole;
   size_t total = 0;
   for (int i = 0; i < ns; ++i) {
@@ -247,8 +253,8 @@ size_t split_workspace(const vtd_config* c, const vtd_dims& d) {
 }
 struct SideStream {
   int device = -1;
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
+  hipStream_t s[kMaxSplit - 1] = {};
+  hipEvent_t fork = nullptr, join[kMaxSplit - 1] = {};
 };
 // per-device side stream + fork/join events, created on the first eager call (never
 // during a HIP-graph capture: a captured first call runs unsplit)
@@ -259,14 +265,15 @@ SideStream* side_stream(hipStream_t st) {
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
   std::lock_guard<std::mutex> g(mu);
   SideStream& ss = per_dev[dev];
-  if (ss.s) return &ss;
+  if (ss.device == dev) return &ss;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
     return nullptr;
-  if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-  if (hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess)
-    return nullptr;
+  if (hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
+  for (int i = 0; i < kMaxSplit - 1; ++i)
+    if (hipStreamCreateWithFlags(&ss.s[i], hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&ss.join[i], hipEventDisableTiming) != hipSuccess)
+      return nullptr;
   ss.device = dev;
   return &ss;
 }
@@ -315,27 +322,32 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
     if (ns == 1) return forward_impl(cfg, w, images, logits, dets, ws, st);
     // no side stream (first call under capture): the halves run in order on `st`
   }
-  const vtd_config c0 = sub_config(cfg, 0, 2), c1 = sub_config(cfg, 1, 2);
-  vtd_dims d0;
-  rc = derive(&c0, &d0);
-  if (rc) return rc;
   const size_t img = (size_t)cfg->image_h * cfg->image_w * cfg->channels;
-  const size_t out0 = (size_t)c0.batch * VTD_MAX_DETECT * 6;
-  hipStream_t s1 = st;
-  if (side) {
-    VTD_HIP(hipEventRecord(side->fork, st));
-    VTD_HIP(hipStreamWaitEvent(side->s, side->fork, 0));
-    s1 = side->s;
+  if (side) VTD_HIP(hipEventRecord(side->fork, st));
+  int64_t b0 = 0;
+  size_t ws_off = 0;
+  for (int part = 0; part < ns; ++part) {
+    const vtd_config cp = sub_config(cfg, part, ns);
+    vtd_dims dp;
+    rc = derive(&cp, &dp);
+    if (rc) return rc;
+    hipStream_t sp = st;
+    if (side && part > 0) {
+      sp = side->s[part - 1];
+      VTD_HIP(hipStreamWaitEvent(sp, side->fork, 0));
+    }
+    const size_t out_off = (size_t)b0 * VTD_MAX_DETECT * 6;
+    rc = forward_impl(&cp, w, images + b0 * img, logits + out_off,
+                      dets ? dets + out_off : nullptr, ws + ws_off, sp);
+    if (rc) return rc;
+    b0 += cp.batch;
+    ws_off += make_plan(&cp, dp).total;
   }
-  rc = forward_impl(&c0, w, images, logits, dets, ws, st);
-  if (rc) return rc;
-  rc = forward_impl(&c1, w, images + c0.batch * img, logits + out0, dets ? dets + out0 : nullptr,
-                    ws + make_plan(&c0, d0).total, s1);
-  if (rc) return rc;
-  if (side) {
-    VTD_HIP(hipEventRecord(side->join, side->s));
-    VTD_HIP(hipStreamWaitEvent(st, side->join, 0));
-  }
+  if (side)
+    for (int part = 1; part < ns; ++part) {
+      VTD_HIP(hipEventRecord(side->join[part - 1], side->s[part - 1]));
+      VTD_HIP(hipStreamWaitEvent(st, side->join[part - 1], 0));
+    }
   return VTD_OK;
 }
 }  // extern "C"
