@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define VTD_ABI_VERSION 7
+#define VTD_ABI_VERSION 8
 #define VTD_KALIGN 64          /* K / row padding granule, elements              */
 #define VTD_MAX_MLP 16         /* max encoder_mlp_quantities                     */
 #define VTD_MAX_HEAD 64        /* max mlp_head layers * repeats                   */
@@ -244,6 +244,15 @@ int vtd_fold_layernorm(const float* w32_dev, int N, int K, int ldw, const float*
  * out [B*N][ldo] at column h*dkp.  dkp in {32, 64, 128}; scale = 1/sqrt(key_dim). */
 int vtd_attention(const void* qkv_dev, int B, int N, int heads, int dkp, int ldqkv,
                   float scale, void* out_dev, int ldo, int dtype, void* stream);
+
+/* vtd_attention (bf16 operands) with the output written as the MX-fp8 A operand of the
+ * attention-output Dense (VTD_FP8 mode): q_dev [B*N][ldq] e4m3 bytes, s_dev
+ * [heads*dkp/128][s_rows][4] E8M0 scales (the vtd_quantize_mx8 layout); byte-identical to
+ * vtd_attention (bf16 out) followed by vtd_quantize_mx8. heads*dkp % 128 == 0, ldq % 16 == 0,
+ * s_rows >= B*N. */
+int vtd_attention_mx8(const void* qkv_dev, int B, int N, int heads, int dkp, int ldqkv,
+                      float scale, uint8_t* q_dev, int ldq, uint8_t* s_dev, int64_t s_rows,
+                      void* stream);
 
 /* transform_predictions (vtd.py:586-647): logits fp32 [n][6] -> detections fp32
  * [sigmoid, sigmoid*79, clip(sigmoid)*608 x4]. */

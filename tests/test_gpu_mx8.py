@@ -154,3 +154,27 @@ def test_gemm_mx8_fp8_output_equals_quantized_bf16_output(L, cuda, M, N, K, act)
     torch.cuda.synchronize()
     assert torch.equal(q, q_ref)
     assert torch.equal(s, s_ref)
+
+
+@pytest.mark.parametrize("B,N,H,dkp", [(2, 196, 12, 64), (1, 576, 16, 64), (3, 100, 4, 32),
+                                       (1, 70, 2, 128)])
+def test_attention_mx8_equals_attention_then_quantize(L, cuda, B, N, H, dkp):
+    """The attention kernel's MX-fp8 epilogue (the VTD_FP8 attention-output operand) writes
+    exactly the bytes of vtd_attention (bf16 out) followed by vtd_quantize_mx8."""
+    g = torch.Generator(device=cuda).manual_seed(B * N + H)
+    ld = 3 * H * dkp
+    qkv = (torch.randn(B * N, ld, generator=g, device=cuda) * 1.5).to(torch.bfloat16)
+    inner, rows = H * dkp, B * N
+    scale = 1.0 / math.sqrt(dkp)
+    o = torch.zeros(rows, inner, device=cuda, dtype=torch.bfloat16)
+    L.check(L.lib.vtd_attention(qkv.data_ptr(), B, N, H, dkp, ld, scale, o.data_ptr(), inner,
+                                L.BF16, L.stream_ptr()), "attention")
+    q_ref, s_ref, s_rows = _quantize(L, o, inner)
+    q = torch.full((rows, inner), 0x7f, dtype=torch.uint8, device=cuda)
+    s = torch.full_like(s_ref, 0xff)
+    L.check(L.lib.vtd_attention_mx8(qkv.data_ptr(), B, N, H, dkp, ld, scale, q.data_ptr(), inner,
+                                    s.data_ptr(), s_rows, L.stream_ptr()), "attention_mx8")
+    torch.cuda.synchronize()
+    assert torch.equal(q, q_ref)
+    v = s.view(inner // 128, s_rows, 4)[:, :rows]
+    assert torch.equal(v, s_ref.view(inner // 128, s_rows, 4)[:, :rows])

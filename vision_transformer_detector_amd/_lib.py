@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede loading libvtd.so, see module doc)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvtd.so")
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 KALIGN = 64
 MAX_MLP = 16
 MAX_HEAD = 64
@@ -106,6 +106,8 @@ SIGNATURES = {
                                    c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "vtd_attention": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_float,
                               c_void_p, c_int, c_int, c_void_p]),
+    "vtd_attention_mx8": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p,
+                                  c_int, c_void_p, c_int64, c_void_p]),
     "vtd_decode": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "vtd_decode_detections": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                       c_float, c_float, c_void_p]),

@@ -244,10 +244,15 @@ struct AttnBf16Cfg {
   static constexpr int DB = DKP / 32;
 };
 
-template <int DKP, int NWG>
+// MX8: the output is written as the MX-fp8 A operand of the attention-output GEMM (VTD_FP8
+// mode) instead of bf16: per 32-column block (lanes l and l ^ 32 of one query hold 16 values
+// each) the amax of the bf16-rounded values -> E8M0 scale -> e4m3 bytes, exactly what
+// vtd_quantize_mx8 makes of the bf16 output (layout in vtd_mx8.hip: q[row][ldo] bytes,
+// s[k / 128][s_rows][4]).
+template <int DKP, int NWG, bool MX8 = false>
 __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void attention_bf16_kernel(
     const bf16_t* __restrict__ qkv, int N, int heads, int ldqkv, float scale_log2,
-    bf16_t* __restrict__ out, int ldo) {
+    bf16_t* __restrict__ out, int ldo, uint8_t* __restrict__ s8 = nullptr, int64_t s_rows = 0) {
   using C = AttnBf16Cfg<DKP>;
   typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -416,7 +421,32 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
   if (!active) return;
   const float inv = 1.f / (l_run + __shfl_xor(l_run, 32));
   const int q = q0 + col;
-  if (q >= N) return;
+  if (q >= N) return;          // lanes l and l ^ 32 hold the same query: both leave or stay
+  if constexpr (MX8) {
+    uint8_t* qp = reinterpret_cast<uint8_t*>(out) + (row0 + q) * (int64_t)ldo + h * DKP;
+#pragma unroll
+    for (int db = 0; db < C::DB; ++db) {
+      float v[16];
+      float amax = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        v[i] = bf16_round(o[db][i] * inv);
+        amax = fmaxf(amax, fabsf(v[i]));
+      }
+      amax = fmaxf(amax, __shfl_xor(amax, 32));
+      const int E = mx8_exponent(amax);
+      const float sinv = __uint_as_float((uint32_t)(127 - E) << 23);     // 2^-E, exact
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<uint32_t*>(qp + db * 32 + 8 * g + 4 * half) =
+            mx8_pack4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3], sinv);
+      if (half == 0) {
+        const int k0 = h * DKP + db * 32;
+        s8[((int64_t)(k0 >> 7) * s_rows + row0 + q) * 4 + ((k0 >> 5) & 3)] = (uint8_t)(E + 127);
+      }
+    }
+    return;
+  }
   bf16_t* op = out + (row0 + q) * ldo + h * DKP;
 #pragma unroll
   for (int db = 0; db < C::DB; ++db)
@@ -429,21 +459,23 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
     }
 }
 
-template <int DKP, int NWG>
+template <int DKP, int NWG, bool MX8 = false>
 int launch_bf16_v2(const void* qkv, int B, int N, int heads, int ldqkv, float scale,
-                   void* out, int ldo, hipStream_t stream) {
+                   void* out, int ldo, hipStream_t stream, uint8_t* s8 = nullptr,
+                   int64_t s_rows = 0) {
   using C = AttnBf16Cfg<DKP>;
   const int nq = (N + 31) / 32;
   dim3 grid((nq + NWG - 1) / NWG, heads, B);
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_bf16_kernel<DKP, NWG>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 2 * C::BUF);
+    (void)hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&attention_bf16_kernel<DKP, NWG, MX8>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, 2 * C::BUF);
     attr_set = true;
   }
-  hipLaunchKernelGGL((attention_bf16_kernel<DKP, NWG>), grid, dim3(64 * NWG), 2 * C::BUF,
+  hipLaunchKernelGGL((attention_bf16_kernel<DKP, NWG, MX8>), grid, dim3(64 * NWG), 2 * C::BUF,
                      stream, static_cast<const bf16_t*>(qkv), N, heads, ldqkv,
-                     scale * 1.4426950408889634f, static_cast<bf16_t*>(out), ldo);
+                     scale * 1.4426950408889634f, static_cast<bf16_t*>(out), ldo, s8, s_rows);
   VTD_LAUNCH_CHECK("attention_bf16");
   return VTD_OK;
 }
@@ -507,7 +539,34 @@ int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqk
   return launch<float, 128>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
 }
 
+int attention_mx8_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqkv,
+                         float scale, uint8_t* q, int ldq, uint8_t* s, int64_t s_rows,
+                         hipStream_t stream, double flops) {
+  VTD_CHECK_ARG(qkv && q && s, "attention_mx8: null pointer");
+  VTD_CHECK_ARG(B > 0 && N > 0 && heads > 0, "attention_mx8: bad B/N/heads");
+  VTD_CHECK_ARG(dkp == 32 || dkp == 64 || dkp == 128, "attention_mx8: dkp must be 32/64/128");
+  VTD_CHECK_ARG((heads * dkp) % 128 == 0,
+                "attention_mx8: heads * dkp must be a multiple of 128 (whole MX K-steps)");
+  VTD_CHECK_ARG(ldqkv >= 3 * heads * dkp && ldqkv % 8 == 0 && ldq >= heads * dkp && ldq % 16 == 0,
+                "attention_mx8: leading dimensions (ldqkv % 8, ldq % 16)");
+  VTD_CHECK_ARG(s_rows >= (int64_t)B * N, "attention_mx8: s_rows < B * N");
+  ProfScope ps(stream, PROF_ATTN,
+               flops > 0 ? flops : 4.0 * B * heads * (double)N * N * dkp);
+  if (dkp == 32)
+    return launch_bf16_v2<32, 8, true>(qkv, B, N, heads, ldqkv, scale, q, ldq, stream, s, s_rows);
+  if (dkp == 64)
+    return launch_bf16_v2<64, 8, true>(qkv, B, N, heads, ldqkv, scale, q, ldq, stream, s, s_rows);
+  return launch_bf16_v2<128, 8, true>(qkv, B, N, heads, ldqkv, scale, q, ldq, stream, s, s_rows);
+}
+
 }  // namespace vtd
+
+extern "C" int vtd_attention_mx8(const void* qkv_dev, int B, int N, int heads, int dkp,
+                                 int ldqkv, float scale, uint8_t* q_dev, int ldq, uint8_t* s_dev,
+                                 int64_t s_rows, void* stream) {
+  return vtd::attention_mx8_launch(qkv_dev, B, N, heads, dkp, ldqkv, scale, q_dev, ldq, s_dev,
+                                   s_rows, static_cast<hipStream_t>(stream), 0.0);
+}
 
 extern "C" int vtd_attention(const void* qkv_dev, int B, int N, int heads, int dkp,
                              int ldqkv, float scale, void* out_dev, int ldo, int dtype,

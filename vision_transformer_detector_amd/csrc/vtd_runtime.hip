@@ -25,6 +25,9 @@ bool gemm_emits_stats(int M, int N, int dtype, const vtd_epilogue* e);
 int patches_launch(const float* img, int B, int H, int W, int C, int p, void* out, int ldo,
                    int dtype, hipStream_t st);
 int decode_launch(const float* logits, int64_t n, float* dets, hipStream_t st);
+int attention_mx8_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqkv,
+                         float scale, uint8_t* q, int ldq, uint8_t* s, int64_t s_rows,
+                         hipStream_t stream, double flops);
 int quantize_mx8_launch(const void* x, int x_dtype, int64_t rows, int K, int ldx, int Kq,
                         uint8_t* q, int ldq, uint8_t* s, int64_t s_rows, hipStream_t st);
 int layernorm_mx8_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx,
@@ -471,9 +474,13 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
                : enc_gemm(d.qkv_p, Dp, a1, L.w_qkv, L.s_qkv, &e, fl);
       if (rc) return rc;
     }
-    rc = attention_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale, attn,
-                          d.inner_p, dt, st,
-                          4.0 * B * cfg->num_heads * (double)N * N * cfg->key_dim);
+    // VTD_FP8 with whole MX K-steps: attention writes the output GEMM's MX-fp8 operand
+    const bool attn_mx8 = fp8 && d.inner_p % 128 == 0 && k8_of(d.inner_p) == d.inner_p;
+    const double attn_flops = 4.0 * B * cfg->num_heads * (double)N * N * cfg->key_dim;
+    rc = attn_mx8 ? attention_mx8_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale,
+                                         q8, d.inner_p, s8, P.s8_rows, st, attn_flops)
+                  : attention_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale,
+                                     attn, d.inner_p, dt, st, attn_flops);
     if (rc) return rc;
     {
       vtd_epilogue e{};
@@ -481,8 +488,9 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
       e.resid = x; e.ldr = Dp;
       e.out = x; e.ldo = Dp; e.out_dtype = rdt;
       emit_stats(e, L.ln2_colsum != nullptr);
-      rc = enc_gemm(Dp, d.inner_p, attn, L.w_out, L.s_out, &e,
-                    2.0 * fR * cfg->num_heads * cfg->key_dim * D);
+      const double fl = 2.0 * fR * cfg->num_heads * cfg->key_dim * D;
+      rc = attn_mx8 ? mx_gemm(Dp, d.inner_p, q8, s8, L.w_out, L.s_out, &e, fl)
+                    : enc_gemm(Dp, d.inner_p, attn, L.w_out, L.s_out, &e, fl);
       if (rc) return rc;
     }
     const void* a = h;
