@@ -44,7 +44,7 @@ def main():
         us = e0.elapsed_time(e1) * 1e3 / a.reps
         nbytes = B * (h * w * 3 + th * tw * 12)
         print(json.dumps({"op": "resize_with_pad",
-                          "variant": int(os.environ.get("VTD_RESIZE_VARIANT", "1")), "batch": B, "source": [h, w],
+                          "batch": B, "source": [h, w],
                           "target": [th, tw], "us": round(us, 1),
                           "images_per_s": round(B / us * 1e6),
                           "gbps": round(nbytes / us / 1e3, 1), "peak_gbps": 8000,
