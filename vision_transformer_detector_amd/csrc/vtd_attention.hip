@@ -421,6 +421,29 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
   if (!active) return;
   const float inv = 1.f / (l_run + __shfl_xor(l_run, 32));
   const int q = q0 + col;
+  if constexpr (!MX8 && DKP == 64) {
+    // bf16 output through LDS (free after the loop's last barrier): a lane holds 16-B
+    // pieces of one query row spread over 8 columns groups, so direct stores write 16 B
+    // per row per instruction; restaged (row stride 144 B: the 16-lane groups of the
+    // 8-B writes hit distinct banks) every store instruction writes 8 whole 128-B rows.
+    char* wst = smem + wave * (32 * 144);
+#pragma unroll
+    for (int db = 0; db < C::DB; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<uint2*>(wst + col * 144 + (db * 32 + 8 * g + 4 * half) * 2) =
+            uint2{pack_bf16x2(o[db][4 * g + 0] * inv, o[db][4 * g + 1] * inv),
+                  pack_bf16x2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv)};
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // wave-local: own writes landed
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {
+      const int r = pass * 8 + (lane >> 3), ch = lane & 7;
+      if (q0 + r < N)
+        *reinterpret_cast<i32x4*>(out + (row0 + q0 + r) * ldo + h * DKP + ch * 8) =
+            *reinterpret_cast<const i32x4*>(wst + r * 144 + ch * 16);
+    }
+    return;
+  }
   if (q >= N) return;          // lanes l and l ^ 32 hold the same query: both leave or stay
   if constexpr (MX8) {
     uint8_t* qp = reinterpret_cast<uint8_t*>(out) + (row0 + q) * (int64_t)ldo + h * DKP;
