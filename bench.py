@@ -3,7 +3,11 @@
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--dtype bf16|f32|fp8]
                   [--preset vit_b16_224|vit_b16_640|vit_l16_384|c1]
-  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+  N > 1 either under a launcher (one rank per GPU, RANK/LOCAL_RANK/WORLD_SIZE from env):
+      python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+  or standalone: `python bench.py --gpus N` starts the N rank processes itself (before
+  anything touches the GPU) with MASTER_ADDR=127.0.0.1 and waits for them.
+  --dry-run: the launcher and the all-gather on CPU (gloo), no GPU and no forward.
 
 One step = one forward of B images per rank (images already resident in HBM) + the
 device-side decode (transform_predictions) + the RCCL all-gather of the (B, 17, 6)
@@ -13,6 +17,8 @@ Prints ONE JSON line on rank 0.
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -123,9 +129,92 @@ def cpu_baseline(model, kw, shape, seconds=12.0):
                       f"preset on the fp32 torch-CPU restatement, {threads} threads"}
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """`--gpus N` with no launcher around us: start N rank processes of this same command
+    line (rank r on GPU r, rendezvous on 127.0.0.1) and wait for them.  Runs before this
+    process makes any GPU call.  If a rank fails, the others (which would wait in a
+    collective forever) are terminated by their own handles.  Returns the exit code."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] +
+                                      sys.argv[1:], env=env))
+    code = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and code == 0:
+                code = rc if rc > 0 else 128 - rc
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+    return code
+
+
+def dry_run(args, world, rank):
+    """CPU rehearsal of the multi-rank path (gloo): the launcher, the rendezvous, the
+    barrier / max-over-ranks timing and the all-gather of (B, 17, 6) detections, without
+    the GPU forward.  Prints the same JSON line shape with `value` = gathered images/s."""
+    from vision_transformer_detector_amd.distributed import all_gather_detections
+    if world > 1:
+        dist.init_process_group("gloo")
+    B = args.batch
+    dets = torch.full((B, 17, 6), float(rank))
+    for _ in range(args.warmup):
+        out = all_gather_detections(dets, world * B) if world > 1 else dets
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = all_gather_detections(dets, world * B) if world > 1 else dets
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ranks_ok = out.shape[0] == world * B and all(
+        bool((out[r * B:(r + 1) * B] == r).all()) for r in range(world))
+    if rank == 0:
+        print(json.dumps({
+            "metric": "dry-run: all-gather of detections only (no GPU forward)",
+            "value": round(world * B * args.steps / max(elapsed, 1e-9), 2),
+            "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / max(1, args.steps), 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32", "data": "synthetic", "gather_rank_order_ok": ranks_ok,
+            "config": {"workload": "dry-run (gloo, CPU)", "per_gpu_batch": B,
+                       "global_batch": world * B, "parallelism": f"dp{world}"}}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if not ranks_ok:
+        raise SystemExit(f"rank {rank}: all-gather returned the wrong rank order")
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default: WORLD_SIZE from the launcher, else 1")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal: launcher + gloo all-gather, no GPU forward")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256, help="images per GPU")
@@ -141,9 +230,19 @@ def main():
     args = ap.parse_args()
     os.environ["VTD_STREAMS"] = str(args.streams)      # read once by libvtd.so
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus is not None and args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus))          # no GPU call has happened yet
+        world = 1
+    else:
+        world = int(os.environ["WORLD_SIZE"])
+        if args.gpus is not None and args.gpus != world:
+            raise SystemExit(f"--gpus {args.gpus} disagrees with WORLD_SIZE={world} "
+                             "from the launcher")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:

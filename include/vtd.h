@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define VTD_ABI_VERSION 8
+#define VTD_ABI_VERSION 9
 #define VTD_KALIGN 64          /* K / row padding granule, elements              */
 #define VTD_MAX_MLP 16         /* max encoder_mlp_quantities                     */
 #define VTD_MAX_HEAD 64        /* max mlp_head layers * repeats                   */
@@ -177,8 +177,9 @@ typedef struct vtd_epilogue {
    * (acc - mean * colsum[n]) * rstd before bias / act.  Both NULL: no fold. */
   const float* lnstat; const float* colsum;
   /* Partial LayerNorm statistics of the output (the fold path's producer side): for row m
-   * and 64-column block b, statout[2 (m stat_ld + b)] = sum and [.. + 1] = sum of squares
-   * of the stored bf16 values.  Only on full 256 x 256 tiles of the bf16 fast epilogues
+   * and 64-column block b, statout[2 (m stat_ld + b)] = mean and [.. + 1] = sum of squared
+   * deviations from that mean, of the block's 64 stored bf16 values (centred partials:
+   * exact whatever |mean| / std).  Only on full 256 x 256 tiles of the bf16 fast epilogues
    * (else vtd_gemm returns VTD_ERR_UNSUPPORTED); NULL: none. */
   float* statout; int stat_ld;
   /* out_dtype VTD_FP8 (vtd_gemm_mx8 only, every tile full: M % 256 == N % 256 == 0): the
@@ -223,8 +224,9 @@ int vtd_layernorm(const void* x_dev, int x_dtype, int64_t rows, int D, int ldx,
 int vtd_layernorm_stats(const void* x_dev, int x_dtype, int64_t rows, int D, int ldx,
                         float eps, float* stat_dev, void* stream);
 
-/* (mean, rstd) per row from the partial sums a producer GEMM wrote (vtd_epilogue.statout,
- * `slots` 64-column blocks per row): one-pass variance sum(x^2)/D - mean^2 in fp32. */
+/* (mean, rstd) per row from the centred partials a producer GEMM wrote
+ * (vtd_epilogue.statout, `slots` 64-column blocks per row, D == 64 * slots): Chan's merge
+ * of the block (mean, M2) pairs in fp32, no one-pass sum(x^2) - mean^2 cancellation. */
 int vtd_layernorm_stats_finalize(const float* partial_dev, int64_t rows, int slots, int D,
                                  float eps, float* stat_dev, void* stream);
 

@@ -7,6 +7,7 @@ they are generated.  Inputs and weights are regenerated from seeds (numpy PCG64 
 platform-stable) for the large C1/C2 cases; tiny cases store everything explicitly.
 
 Run:  python tests/golden/make_golden.py [seeded case names ...]
+      python tests/golden/make_golden.py batched [batched case names ...]
 """
 import hashlib
 import json
@@ -58,6 +59,41 @@ SEEDED = {
     # C5: ViT-L/16 preset at 384x384 (D 1024, 16 heads, 24 layers)
     "c5_vitl16_384_b1": dict(kw="vit_l16_384", batch=1, wseed=0, iseed=1, letterbox=True),
 }
+
+# Multi-image cases for the batched parity tests (tests/test_gpu_batch_parity.py): the
+# same weights as the b1 case of the preset, `n` distinct images from one seed, each
+# image's fp64 logits stored.  The GPU test places them among random filler images in a
+# batch of the config's real size (C2 B=256 / 64, C3 B=32, C5 B=128), so the timed
+# kernels (256-tile GEMMs, producer LayerNorm statistics, two streams) are what is checked.
+BATCHED = {
+    "c2_vitb16_imgs8": dict(kw="vit_b16_224", n=8, wseed=0, iseed=100, letterbox=True),
+    "c3_vitb16_640_imgs3": dict(kw="vit_b16_640", n=3, wseed=0, iseed=101, letterbox=True),
+    "c5_vitl16_384_imgs3": dict(kw="vit_l16_384", n=3, wseed=0, iseed=102, letterbox=True),
+}
+
+
+def make_batched(names=None):
+    from vision_transformer_detector_amd import presets
+    path = os.path.join(HERE, "batched_forward.json")
+    out = json.load(open(path)) if os.path.exists(path) else {}
+    for name, c in BATCHED.items():
+        if names and name not in names:
+            continue
+        kw = dict(presets.PRESETS[c["kw"]])
+        shape = V.resolve_kwargs(**kw)["input_shape"]
+        w = V.init_weights(seed=c["wseed"], perturb=0.02, **kw)
+        x = V.synthetic_images(c["n"], shape, seed=c["iseed"], letterbox=c["letterbox"])
+        ys = [V.forward(w, x[i:i + 1], **kw)[0] for i in range(c["n"])]
+        y2 = T.TorchCpuDetector(w, dtype=torch.float64, **kw)(x[:1]).numpy()[0]
+        assert np.abs(ys[0] - y2).max() < 1e-12, name
+        out[name] = dict(preset=c["kw"], kwargs=kw, n=c["n"], weight_seed=c["wseed"],
+                         perturb=0.02, image_seed=c["iseed"], letterbox=c["letterbox"],
+                         images_sha256=digest(x),
+                         weights_sha256=digest(np.concatenate([v.ravel() for v in w.values()])),
+                         logits=[y.tolist() for y in ys])
+        print(name, float(max(np.abs(y).max() for y in ys)), flush=True)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
 
 
 def digest(a):
@@ -112,4 +148,7 @@ def main(only=None):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:] or None)
+    if sys.argv[1:2] == ["batched"]:
+        make_batched(sys.argv[2:] or None)
+    else:
+        main(sys.argv[1:] or None)

@@ -98,3 +98,35 @@ def test_data_parallel_gather_matches_single_process(world, batch):
         np.testing.assert_array_equal(out, out2)
         np.testing.assert_allclose(out, full, rtol=0, atol=1e-6)
         assert (kern == 10.0).all()            # everyone now holds rank 0's weights
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_launches_ranks_itself(world):
+    """`python bench.py --gpus N` with no launcher starts N rank processes (the driver's
+    command shape); --dry-run rehearses the rendezvous, max-over-ranks timing and the
+    all-gather on gloo.  rank 0 prints one JSON line with n_gpus = N."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(world),
+                        "--dry-run", "--steps", "3", "--warmup", "1", "--batch", "5"],
+                       capture_output=True, text=True, timeout=180, env=env, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == world and out["config"]["global_batch"] == 5 * world
+    assert out["gather_rank_order_ok"] is True
+
+
+def test_bench_rejects_gpus_world_mismatch():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4",
+                        "--dry-run"], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "disagrees" in r.stderr

@@ -98,6 +98,16 @@ def test_predict_and_decode_api(vtd, cuda):
     assert ok
     d = vtd.transform_predictions(torch.from_numpy(y).to(cuda)).cpu().numpy()
     assert np.abs(d - V.transform_predictions(y)).max() < 1e-3
+    # the reference's own usage (vtd.py:1341, 2447): decode whatever predict returned
+    dn = vtd.transform_predictions(model.predict(x, batch_size=1))
+    assert isinstance(dn, np.ndarray) and dn.dtype == np.float32
+    np.testing.assert_array_equal(dn, d)
+    dc = vtd.transform_predictions(torch.from_numpy(y))           # CPU tensor in, CPU out
+    assert torch.is_tensor(dc) and dc.device.type == "cpu"
+    np.testing.assert_array_equal(dc.numpy(), d)
+    dets, cat, valid = vtd.decode_detections(y)
+    assert isinstance(dets, np.ndarray) and cat.dtype == np.int32 and valid.dtype == bool
+    np.testing.assert_array_equal(dets, d)
     # get_weights round-trips in Keras order
     names = model.weight_names()
     assert names == list(V.weight_shapes(**kw))
@@ -193,3 +203,30 @@ def test_two_stream_split_graph_capture(vtd, cuda):
     graph.replay()
     torch.cuda.synchronize()
     assert torch.equal(buf, eager)
+
+
+def test_bf16_with_f32_residual_stream_env(cuda):
+    """VTD_RESID_F32=1 (f32 residual stream in the bf16 mode, an A/B switch read once by
+    libvtd.so, hence a child process) must not combine with the LayerNorm fold, whose
+    GEMMs read the stream as their bf16 operand: the model packs unfolded weights and the
+    bf16 golden still holds."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import sys, json, numpy as np, torch\n"
+        f"sys.path.insert(0, {root!r})\n"
+        "import vision_transformer_detector_amd as vtd\n"
+        "from tests.test_gpu_model import load_tiny, within\n"
+        "for name in ('tiny_mish', 'tiny_gelu'):\n"
+        "    kw, w, x, logits, _ = load_tiny(name)\n"
+        "    m = vtd.create_vision_transformer_detector(**kw, dtype='bfloat16')\n"
+        "    m.set_weights(w)\n"
+        "    y = m(torch.from_numpy(x).cuda()).cpu().numpy()\n"
+        "    ok, rel = within(y, logits, 3e-2)\n"
+        "    print(name, ok, rel)\n"
+        "    assert ok, (name, rel)\n")
+    env = dict(os.environ, VTD_RESID_F32="1")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                       timeout=300, env=env, cwd=root)
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]

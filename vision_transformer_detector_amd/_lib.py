@@ -14,7 +14,7 @@ import torch  # noqa: F401  (must precede loading libvtd.so, see module doc)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvtd.so")
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 KALIGN = 64
 MAX_MLP = 16
 MAX_HEAD = 64

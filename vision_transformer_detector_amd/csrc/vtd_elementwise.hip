@@ -301,23 +301,34 @@ void ln_stats_dispatch(const void* xv, int64_t rows, int D, int ldx, float eps, 
 #undef VTD_LS
 }
 
-// (mean, rstd) per row from a producer GEMM's partial (sum, sum of squares) per 64-column
-// block: one thread per row.
+// (mean, rstd) per row from a producer GEMM's centred partials per 64-column block
+// (block mean m_b, sum of squared deviations M2_b; every block holds 64 valid columns):
+// Chan et al.'s pairwise merge for equal counts, mean = sum_b m_b / slots and
+// M2 = sum_b M2_b + 64 sum_b (m_b - mean)^2, with the block means taken relative to the
+// first one.  No large nearly-equal terms are subtracted, whatever |mean| / std is.
+// One thread per row.
 __global__ __launch_bounds__(256) void ln_stats_finalize_kernel(const float2* __restrict__ part,
                                                                 int64_t rows, int slots, int D,
                                                                 float eps,
                                                                 float2* __restrict__ stat) {
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (r >= rows) return;
-  float s = 0.f, q = 0.f;
+  const float2* pr = part + r * slots;
+  const float m0 = pr[0].x;
+  float ds = 0.f, q = 0.f;
   for (int b = 0; b < slots; ++b) {
-    const float2 t = part[r * slots + b];
-    s += t.x;
+    const float2 t = pr[b];
+    ds += t.x - m0;
     q += t.y;
   }
-  const float mean = s / D;
-  const float var = fmaxf(q / D - mean * mean, 0.f);
-  stat[r] = float2{mean, 1.f / sqrtf(var + eps)};
+  const float dmean = ds / slots;
+  float between = 0.f;
+  for (int b = 0; b < slots; ++b) {
+    const float dv = (pr[b].x - m0) - dmean;
+    between += dv * dv;
+  }
+  const float var = (q + 64.f * between) / D;
+  stat[r] = float2{m0 + dmean, 1.f / sqrtf(var + eps)};
 }
 
 // LayerNorm fold of one consumer Dense layer (one-time weight preparation): one wave per
@@ -546,7 +557,8 @@ int ln_stats_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx, fl
 int ln_stats_finalize_launch(const float* part, int64_t rows, int slots, int D, float eps,
                              float* stat, hipStream_t st) {
   VTD_CHECK_ARG(part && stat, "layernorm_stats_finalize: null pointer");
-  VTD_CHECK_ARG(rows > 0 && slots > 0 && D > 0, "layernorm_stats_finalize: bad shape");
+  VTD_CHECK_ARG(rows > 0 && slots > 0 && D == 64 * slots,
+                "layernorm_stats_finalize: bad shape (D must be 64 * slots: every block full)");
   VTD_CHECK_ARG(reinterpret_cast<uintptr_t>(part) % 8 == 0 && reinterpret_cast<uintptr_t>(stat) % 8 == 0,
                 "layernorm_stats_finalize: alignment");
   ProfScope ps(st, PROF_LN, 0.0);

@@ -37,7 +37,9 @@ struct EpiArgs {
   // per column colsum[n] = sum_k Bt[n][k]; acc -> (acc - mean * colsum) * rstd first
   const float2* lnstat; const float* colsum;
   // partial LayerNorm statistics of the stored bf16 rows (fold path producer): per row m
-  // and 64-column block b, statout[m * stat_ld + b] = (sum, sum of squares)
+  // and 64-column block b, statout[m * stat_ld + b] = (block mean, sum of squared
+  // deviations from it) -- centred, so rows with |mean| >> std lose nothing (Chan merge in
+  // ln_stats_finalize_kernel)
   float2* statout; int stat_ld;
   // out_dtype VTD_FP8 (MX-fp8 GEMMs, fast epilogue): e4m3 out + E8M0 scales [n/128][s_rows][4]
   uint8_t* sout; int64_t s_rows;
@@ -61,17 +63,31 @@ __device__ __forceinline__ float xsum32(float v) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// (sum, sum of squares) of the 8 bf16 values packed in o
-__device__ __forceinline__ float2 bf16x8_sums(const i32x4& o) {
-  float s = 0.f, q = 0.f;
+// sum of the 8 bf16 values packed in o
+__device__ __forceinline__ float bf16x8_sum(const i32x4& o) {
+  float s = 0.f;
+#pragma unroll
+  for (int w = 0; w < 4; ++w)
+    s += __uint_as_float((uint32_t)o[w] << 16) + __uint_as_float((uint32_t)o[w] & 0xffff0000u);
+  return s;
+}
+// sum of squared deviations from `mean` of the 8 bf16 values packed in o
+__device__ __forceinline__ float bf16x8_m2(const i32x4& o, float mean) {
+  float q = 0.f;
 #pragma unroll
   for (int w = 0; w < 4; ++w) {
-    const float lo = __uint_as_float((uint32_t)o[w] << 16);
-    const float hi = __uint_as_float((uint32_t)o[w] & 0xffff0000u);
-    s += lo + hi;
+    const float lo = __uint_as_float((uint32_t)o[w] << 16) - mean;
+    const float hi = __uint_as_float((uint32_t)o[w] & 0xffff0000u) - mean;
     q += lo * lo + hi * hi;
   }
-  return float2{s, q};
+  return q;
+}
+// total over the 8 consecutive lanes of a half-row, in all 8 lanes: DPP quad xor 1,
+// quad xor 2, then row_half_mirror (lane i <-> 7 - i: the other quad)
+__device__ __forceinline__ float sum8_dpp(float t) {
+  t += dpp_f32<0xB1>(t);
+  t += dpp_f32<0x4E>(t);
+  return t + dpp_f32<0x141>(t);
 }
 
 __device__ __forceinline__ float resid_at(const EpiArgs& e, int64_t i) {
@@ -582,17 +598,12 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
                          (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
         *reinterpret_cast<i32x4*>(static_cast<bf16_t*>(e.out) + idx) = o;
         if (e.statout) {           // the row's 64 columns live in 8 consecutive lanes
-          float2 t = bf16x8_sums(o);
-          // DPP sums (no LDS traffic): quad xor 1, quad xor 2, then row_shr 4 leaves the
-          // 8-lane total in lanes 4..7 of each 8-lane group
-          t.x += dpp_f32<0xB1>(t.x);
-          t.y += dpp_f32<0xB1>(t.y);
-          t.x += dpp_f32<0x4E>(t.x);
-          t.y += dpp_f32<0x4E>(t.y);
-          t.x += dpp_f32<0x114>(t.x);
-          t.y += dpp_f32<0x114>(t.y);
+          // block mean, then the centred sum of squares (DPP sums, no LDS traffic)
+          const float mean = sum8_dpp(bf16x8_sum(o)) * (1.f / 64.f);
+          const float m2 = sum8_dpp(bf16x8_m2(o, mean));
           if ((lane & 7) == 7)
-            e.statout[(int64_t)(m_base + p * PR + row) * e.stat_ld + (n_base >> 6)] = t;
+            e.statout[(int64_t)(m_base + p * PR + row) * e.stat_ld + (n_base >> 6)] =
+                float2{mean, m2};
         }
       } else {
         float* op = static_cast<float*>(e.out) + idx;
@@ -978,7 +989,8 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      float2 tsum = {0.f, 0.f};
+      float tsum = 0.f;
+      i32x4 ob[2];                     // the stored bf16 values (statistics pass below)
 #pragma unroll
       for (int jp = 0; jp < 2; ++jp) {
         f32x4 v0 = acc[i0 + i][2 * jp];
@@ -1005,9 +1017,8 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
                            (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
           *reinterpret_cast<i32x4*>(static_cast<bf16_t*>(e.out) + idx) = o;
           if (e.statout) {
-            const float2 t = bf16x8_sums(o);
-            tsum.x += t.x;
-            tsum.y += t.y;
+            ob[jp] = o;
+            tsum += bf16x8_sum(o);
           }
         } else {
           float* op = static_cast<float*>(e.out) + idx;
@@ -1016,10 +1027,13 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
         }
       }
       if (OUT_BF16 && e.statout) {   // the row's 64 columns: lanes fr, fr + 16, + 32, + 48
-        tsum.x = xsum32(xsum16(tsum.x));
-        tsum.y = xsum32(xsum16(tsum.y));
+        // block mean (lane-swap butterfly: every lane holds it), then the centred sum of
+        // squares of the same stored values
+        const float mean = xsum32(xsum16(tsum)) * (1.f / 64.f);
+        const float m2 = xsum32(xsum16(bf16x8_m2(ob[0], mean) + bf16x8_m2(ob[1], mean)));
         if (fg == 0)
-          e.statout[(int64_t)(m_base + 16 * (i0 + i) + fr) * e.stat_ld + (n_base >> 6)] = tsum;
+          e.statout[(int64_t)(m_base + 16 * (i0 + i) + fr) * e.stat_ld + (n_base >> 6)] =
+              float2{mean, m2};
       }
     }
   }

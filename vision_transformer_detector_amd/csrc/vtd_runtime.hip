@@ -384,7 +384,8 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   }();
   auto emit_stats = [&](vtd_epilogue& e, bool next_fold) {
     partials = false;
-    if (!next_fold || fp8 || dt != VTD_BF16 || !partials_on) return;
+    // centred per-block partials need every 64-column block full of valid columns
+    if (!next_fold || fp8 || dt != VTD_BF16 || !partials_on || D != Dp) return;
     e.statout = pstat; e.stat_ld = nslot;
     partials = gemm_emits_stats(M, Dp, dt, &e);
     if (!partials) { e.statout = nullptr; e.stat_ld = 0; }
@@ -453,6 +454,10 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     const vtd_layer_weights& L = w->layers[i];
     if (fp8 && (L.ln1_colsum || L.ln2_colsum))
       return fail(VTD_ERR_UNSUPPORTED, "forward: LayerNorm fold (ln*_colsum) is not supported in VTD_FP8 mode");
+    // the folded GEMMs take the residual stream x itself as their A operand (read in dt)
+    if (rdt != dt && (L.ln1_colsum || L.ln2_colsum))
+      return fail(VTD_ERR_UNSUPPORTED, "forward: LayerNorm fold (ln*_colsum) needs the residual "
+                                       "stream in the compute dtype (unset VTD_RESID_F32)");
     // LayerNorm 1: its own pass into h, or folded into the query/key/value GEMM
     const void* a1 = h;
     if (L.ln1_colsum) {

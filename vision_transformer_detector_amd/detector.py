@@ -286,7 +286,10 @@ class Model:
         # LayerNorm fold (bf16 mode): LN1 into query/key/value, LN2 into the first MLP
         # layer (vtd_fold_layernorm); the forward then runs vtd_layernorm_stats instead of
         # the LayerNorm passes.  VTD_LN_FOLD=0 keeps the LayerNorm passes (A/B switch).
-        fold = self.dtype == L.BF16 and os.environ.get("VTD_LN_FOLD", "1") != "0"
+        # The folded GEMMs read the residual stream x as their bf16 A operand, so the fold
+        # needs the bf16 stream: VTD_RESID_F32=1 (an f32 stream) turns it off.
+        fold = (self.dtype == L.BF16 and os.environ.get("VTD_LN_FOLD", "1") != "0"
+                and os.environ.get("VTD_RESID_F32", "0") in ("", "0"))
 
         def fold_ln(w32, b32, gamma, beta):
             """(W * diag(gamma), b + W beta, colsum) of a packed fp32 [N_p][K_p] matrix."""
@@ -477,24 +480,40 @@ def create_vision_transformer_detector(
     return Model(kw, dtype=dtype, device=device, seed=seed)
 
 
+def _to_device(inputs, what):
+    """Stage a numpy array / CPU tensor / HIP tensor of shape (..., 6) on the HIP device.
+    Returns (fp32 contiguous device tensor, back) where back(t) hands a result back in the
+    caller's type: numpy in -> numpy out, CPU tensor in -> CPU tensor out.  There is no CPU
+    decode path: without a HIP device this raises."""
+    if torch.is_tensor(inputs):
+        t, back = inputs, ((lambda r: r) if inputs.device.type == "cuda"
+                           else (lambda r: r.cpu()))
+    else:
+        t, back = torch.as_tensor(np.asarray(inputs)), (lambda r: r.cpu().numpy())
+    if t.shape[-1:] != (6,):
+        raise ValueError(f"{what}: expected a (..., 6) input, got {tuple(t.shape)}")
+    if t.device.type != "cuda":
+        if not torch.cuda.is_available():
+            raise RuntimeError(f"{what} runs on the HIP device and none is available")
+        t = t.to(torch.device("cuda", torch.cuda.current_device()))
+    return t.to(torch.float32).contiguous(), back
+
+
 def transform_predictions(inputs):
     """vtd.py:586-647 on a (…, 6) tensor/array: sigmoid; clip the last 4 to [0, 1];
     [objectness, class * (CLASSES - 1), cx * W, cy * H, h * H, w * W] with (H, W) the
-    constant MODEL_IMAGE_SIZE = (608, 608).  Device tensors decode on the GPU via
-    vtd_decode; numpy/CPU inputs are rejected (no CPU path)."""
-    t = inputs if torch.is_tensor(inputs) else torch.as_tensor(np.asarray(inputs))
-    if t.device.type != "cuda":
-        raise ValueError("transform_predictions runs on the HIP device: pass a cuda tensor")
-    if t.shape[-1] != 6:
-        raise ValueError(f"expected last dim 6, got {tuple(t.shape)}")
-    src = t.to(torch.float32).contiguous()
+    constant MODEL_IMAGE_SIZE = (608, 608).  Decodes on the GPU (vtd_decode).  The
+    reference's callers pass whatever `predict` returned (vtd.py:1164, 1341, 2447), so
+    numpy / CPU inputs are staged to the device and the result comes back in the same
+    type (numpy in, numpy out)."""
+    src, back = _to_device(inputs, "transform_predictions")
     out = torch.empty_like(src)
     n = src.numel() // 6
     if n:
         with torch.cuda.device(src.device):
             L.check(L.lib.vtd_decode(src.data_ptr(), n, out.data_ptr(), L.stream_ptr()),
                     "vtd_decode")
-    return out
+    return back(out)
 
 
 def decode_detections(logits, objectness_threshold: float = 0.5,
@@ -502,11 +521,9 @@ def decode_detections(logits, objectness_threshold: float = 0.5,
     """Device-side transform_predictions + thresholded detection test (vtd.py:586-647,
     1359-1384): category = round-half-even(class), confidence = (0.5 - |class -
     category|) / 0.5, valid = objectness > thr and confidence > thr.
-    Returns (dets (..., 6) fp32, category (...) int32, valid (...) bool)."""
-    t = logits if torch.is_tensor(logits) else torch.as_tensor(np.asarray(logits))
-    if t.device.type != "cuda" or t.shape[-1] != 6:
-        raise ValueError("decode_detections needs a (..., 6) tensor on the HIP device")
-    src = t.to(torch.float32).contiguous()
+    Returns (dets (..., 6) fp32, category (...) int32, valid (...) bool) in the caller's
+    type (device tensors for a device input, numpy for numpy, CPU tensors for CPU)."""
+    src, back = _to_device(logits, "decode_detections")
     n = src.numel() // 6
     dets = torch.empty_like(src)
     cat = torch.empty(src.shape[:-1], dtype=torch.int32, device=src.device)
@@ -518,7 +535,7 @@ def decode_detections(logits, objectness_threshold: float = 0.5,
                                                 float(objectness_threshold),
                                                 float(classification_threshold),
                                                 L.stream_ptr()), "vtd_decode_detections")
-    return dets, cat, valid.bool()
+    return back(dets), back(cat), back(valid.bool())
 
 
 def detection_list(dets, category, valid):
