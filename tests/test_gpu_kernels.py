@@ -515,7 +515,7 @@ def test_gemm_statout_and_finalize(L, cuda, N, K, act, resid, offset):
 def test_layernorm_stats_finalize_needs_full_blocks(L, cuda):
     part = torch.zeros(4, 2, 2, device=cuda)
     st = torch.zeros(4, 2, device=cuda)
-    with pytest.raises(L.VtdError):
+    with pytest.raises(ValueError):                # VTD_ERR_INVALID_ARG
         L.check(L.lib.vtd_layernorm_stats_finalize(part.data_ptr(), 4, 2, 100, 1e-3,
                                                    st.data_ptr(), L.stream_ptr()), "finalize")
 

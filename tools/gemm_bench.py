@@ -16,13 +16,16 @@ from vision_transformer_detector_amd import _lib as L  # noqa: E402
 
 SHAPES = {  # name: (M, N, K, act, out_dtype, resid)
     "qkv": (50176, 2304, 768, 0, 1, False),
-    "attn_out": (50176, 768, 768, 0, 0, True),
+    "attn_out": (50176, 768, 768, 0, 1, True),     # bf16 residual stream (the forward's)
     "mlp1": (50176, 3072, 768, 1, 1, False),
     "mlp2": (50176, 1536, 3072, 1, 1, False),
-    "mlp3": (50176, 768, 1536, 1, 0, True),
+    "mlp3": (50176, 768, 1536, 1, 1, True),
     "head1": (4352, 8704, 256, 1, 1, False),
     "head2": (4352, 4352, 8704, 1, 1, False),
     "sq8192": (8192, 8192, 8192, 0, 1, False),
+    # diagnostics: the activation's share of an epilogue (mlp1 / mlp2 without GELU)
+    "mlp1_noact": (50176, 3072, 768, 0, 1, False),
+    "mlp2_noact": (50176, 1536, 3072, 0, 1, False),
 }
 
 

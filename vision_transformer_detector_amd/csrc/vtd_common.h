@@ -118,6 +118,26 @@ __device__ __forceinline__ float act_gelu(float x) {
   const float e = __builtin_amdgcn_exp2f(x * __builtin_fmaf(c1, x * x, c0));
   return x * __builtin_amdgcn_rcpf(1.f + e);
 }
+// Two values at once: the ordinary f32 arithmetic through the packed VALU
+// (v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32, one instruction per pair), the
+// transcendentals one by one (there is no packed v_exp_f32 / v_rcp_f32).  Same operations,
+// same order as the scalar forms above: identical results.  (GELU: 2.5 + 2 transcendental
+// issue slots per value instead of 5 + 2; it is most of the activation layers' epilogue.)
+__device__ __forceinline__ f32x2 act_gelu2(f32x2 x) {
+  constexpr float c0 = -2.f * 0.7978845608028654f * 1.4426950408889634f;
+  constexpr float c1 = c0 * 0.044715f;
+  const f32x2 t = x * __builtin_elementwise_fma(f32x2{c1, c1}, x * x, f32x2{c0, c0});
+  const f32x2 d = f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + 1.f;
+  return x * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+__device__ __forceinline__ f32x2 act_mish2(f32x2 x) {
+  const f32x2 t = x * 1.4426950408889634f;
+  const f32x2 e = f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+  const f32x2 n = e * (e + 2.f);
+  const f32x2 d = n + 2.f;
+  const f32x2 y = x * n * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  return f32x2{x.x > 20.f ? x.x : y.x, x.y > 20.f ? x.y : y.y};
+}
 __device__ __forceinline__ float apply_act(int act, float x) {
   if (act == VTD_ACT_GELU_TANH) return act_gelu(x);
   if (act == VTD_ACT_MISH) return act_mish(x);

@@ -468,6 +468,18 @@ __device__ __forceinline__ float act_ct(float x) {
   else if constexpr (ACT == VTD_ACT_MISH) return act_mish(x);
   else return x;
 }
+// the activation of 8 values (two f32x4), pairwise through the packed VALU
+template <int ACT>
+__device__ __forceinline__ void act_ct8(f32x4& v0, f32x4& v1) {
+  if constexpr (ACT == VTD_ACT_GELU_TANH || ACT == VTD_ACT_MISH) {
+    f32x2 p[4] = {v0.xy, v0.zw, v1.xy, v1.zw};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      p[i] = ACT == VTD_ACT_GELU_TANH ? act_gelu2(p[i]) : act_mish2(p[i]);
+    v0 = f32x4{p[0].x, p[0].y, p[1].x, p[1].y};
+    v1 = f32x4{p[2].x, p[2].y, p[3].x, p[3].y};
+  }
+}
 
 // Rare runtime modes kept on the fast epilogues (one launch per forward each): the
 // position-embedding row add of the patch embedding (vtd.py:305; before the activation,
@@ -554,11 +566,7 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
       v0 += b0;
       v1 += b1;
       if (e.rowadd) epi_rowadd8(e, m_base + p * PR + row, n_base + c8, v0, v1);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v0[j] = act_ct<ACT>(v0[j]);
-        v1[j] = act_ct<ACT>(v1[j]);
-      }
+      act_ct8<ACT>(v0, v1);
       if constexpr (RESID) {
         v0 += rv[it][0];
         v1 += rv[it][1];
@@ -1001,11 +1009,7 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
         v0 += bias[jp][0];
         v1 += bias[jp][1];
         if (e.rowadd) epi_rowadd8(e, mrow, ncol, v0, v1);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v0[r] = act_ct<ACT>(v0[r]);
-          v1[r] = act_ct<ACT>(v1[r]);
-        }
+        act_ct8<ACT>(v0, v1);
         if constexpr (RESID) {
           v0 += rv[i][jp][0];
           v1 += rv[i][jp][1];
@@ -1164,11 +1168,7 @@ __device__ __forceinline__ void epilogue_fast_x(const f32x4 (&acc)[8][4], float*
       const int row = it * 8 + rsub;
       f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + epx(row, c8)) + b0;
       f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + epx(row, c8 + 4)) + b1;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v0[j] = act_ct<ACT>(v0[j]);
-        v1[j] = act_ct<ACT>(v1[j]);
-      }
+      act_ct8<ACT>(v0, v1);
       if constexpr (RESID) {
         v0 += rv[it][0];
         v1 += rv[it][1];

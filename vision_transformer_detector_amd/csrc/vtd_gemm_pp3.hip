@@ -29,6 +29,17 @@ __device__ __forceinline__ float act_ct(float x) {
   else if constexpr (ACT == VTD_ACT_MISH) return act_mish(x);
   else return x;
 }
+template <int ACT>
+__device__ __forceinline__ void act_ct8(f32x4& v0, f32x4& v1) {
+  if constexpr (ACT == VTD_ACT_GELU_TANH || ACT == VTD_ACT_MISH) {
+    f32x2 p[4] = {v0.xy, v0.zw, v1.xy, v1.zw};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      p[i] = ACT == VTD_ACT_GELU_TANH ? act_gelu2(p[i]) : act_mish2(p[i]);
+    v0 = f32x4{p[0].x, p[0].y, p[1].x, p[1].y};
+    v1 = f32x4{p[2].x, p[2].y, p[3].x, p[3].y};
+  }
+}
 
 __device__ __forceinline__ void pp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
@@ -171,11 +182,7 @@ __device__ __forceinline__ void pp3_epilogue(const f32x4 (&acc)[8][4], int lane,
         const int m = m_base + 16 * (i0 + i) + fr;
         f32x4 v0 = acc[i0 + i][2 * jp];             // bias already in the accumulators
         f32x4 v1 = acc[i0 + i][2 * jp + 1];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v0[r] = act_ct<ACT>(v0[r]);
-          v1[r] = act_ct<ACT>(v1[r]);
-        }
+        act_ct8<ACT>(v0, v1);
         if constexpr (RESID) {
           v0 += rv[i][jp][0];
           v1 += rv[i][jp][1];

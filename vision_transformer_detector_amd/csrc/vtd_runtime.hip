@@ -281,8 +281,12 @@ SideStream* side_stream(hipStream_t st) {
   return &ss;
 }
 
+// Stages of one forward: 0 = patches + linear projection, 1..L = encoder layer s - 1,
+// L + 1 = head + decode.  forward_impl runs stages [s_lo, s_hi); `partials` carries
+// "the GEMM that last wrote x emitted LayerNorm partials" from one stage to the next.
 int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* images,
-                 float* logits, float* dets, char* ws, hipStream_t st);
+                 float* logits, float* dets, char* ws, hipStream_t st, int s_lo, int s_hi,
+                 bool& partials);
 }  // namespace
 
 }  // namespace vtd
@@ -321,31 +325,54 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
   char* ws = static_cast<char*>(workspace);
   const int ns = split_count(cfg, d);
   SideStream* side = ns > 1 ? side_stream(st) : nullptr;
+  const int n_stages = cfg->repeat_times + 2;
   if (!side) {
-    if (ns == 1) return forward_impl(cfg, w, images, logits, dets, ws, st);
+    bool partials = false;
+    if (ns == 1) return forward_impl(cfg, w, images, logits, dets, ws, st, 0, n_stages, partials);
     // no side stream (first call under capture): the halves run in order on `st`
   }
   const size_t img = (size_t)cfg->image_h * cfg->image_w * cfg->channels;
   if (side) VTD_HIP(hipEventRecord(side->fork, st));
+  struct Part {
+    vtd_config cfg;
+    const float* images;
+    float* logits;
+    float* dets;
+    char* ws;
+    hipStream_t st;
+    bool partials;
+  } parts[kMaxSplit];
   int64_t b0 = 0;
   size_t ws_off = 0;
   for (int part = 0; part < ns; ++part) {
-    const vtd_config cp = sub_config(cfg, part, ns);
+    Part& P = parts[part];
+    P.cfg = sub_config(cfg, part, ns);
     vtd_dims dp;
-    rc = derive(&cp, &dp);
+    rc = derive(&P.cfg, &dp);
     if (rc) return rc;
-    hipStream_t sp = st;
+    P.st = st;
     if (side && part > 0) {
-      sp = side->s[part - 1];
-      VTD_HIP(hipStreamWaitEvent(sp, side->fork, 0));
+      P.st = side->s[part - 1];
+      VTD_HIP(hipStreamWaitEvent(P.st, side->fork, 0));
     }
     const size_t out_off = (size_t)b0 * VTD_MAX_DETECT * 6;
-    rc = forward_impl(&cp, w, images + b0 * img, logits + out_off,
-                      dets ? dets + out_off : nullptr, ws + ws_off, sp);
-    if (rc) return rc;
-    b0 += cp.batch;
-    ws_off += make_plan(&cp, dp).total;
+    P.images = images + b0 * img;
+    P.logits = logits + out_off;
+    P.dets = dets ? dets + out_off : nullptr;
+    P.ws = ws + ws_off;
+    P.partials = false;
+    b0 += P.cfg.batch;
+    ws_off += make_plan(&P.cfg, dp).total;
   }
+  // Launches are interleaved part by part, one stage (encoder layer) at a time: issuing
+  // all of one part's ~110 launches before the next part's first one left the second
+  // stream idle for the host's whole enqueue time of the first (~0.7 ms at C2, B = 256).
+  for (int s = 0; s < n_stages; ++s)
+    for (int part = 0; part < ns; ++part) {
+      Part& P = parts[part];
+      rc = forward_impl(&P.cfg, w, P.images, P.logits, P.dets, P.ws, P.st, s, s + 1, P.partials);
+      if (rc) return rc;
+    }
   if (side)
     for (int part = 1; part < ns; ++part) {
       VTD_HIP(hipEventRecord(side->join[part - 1], side->s[part - 1]));
@@ -358,7 +385,8 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
 namespace vtd {
 namespace {
 int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* images,
-                 float* logits, float* dets, char* ws, hipStream_t st) {
+                 float* logits, float* dets, char* ws, hipStream_t st, int s_lo, int s_hi,
+                 bool& partials) {
   vtd_dims d;
   int rc = derive(cfg, &d);
   if (rc) return rc;
@@ -376,8 +404,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   float* pstat = reinterpret_cast<float*>(ws + P.pstat);
   const int nslot = Dp / 64;
   // fold path: the GEMM writing x emits partial row statistics when it can (full tiles on
-  // the bf16 fast epilogues); the LayerNorm point then only finalizes them
-  bool partials = false;
+  // the bf16 fast epilogues); the LayerNorm point then only finalizes them (`partials`)
   static const bool partials_on = [] {       // VTD_LN_PARTIALS=0: row-statistics pass
     const char* v = getenv("VTD_LN_PARTIALS");
     return !v || atoi(v) != 0;
@@ -432,6 +459,8 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
                                 P.s8_rows, st);
   };
 
+  const int n_stages = cfg->repeat_times + 2;
+  if (s_lo <= 0 && 0 < s_hi) {
   // ---- ExtractImagePatches + flatten (vtd.py:271-280)
   rc = patches_launch(images, B, cfg->image_h, cfg->image_w, cfg->channels,
                       cfg->patch_size, patches, d.patch_dim_p, dt, st);
@@ -448,9 +477,11 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
                      d.patch_dim_p, dt, &e, st, 2.0 * fR * D * d.patch_dim);
     if (rc) return rc;
   }
+  }
   const int q = cfg->mlp_quantities;
   const float scale = 1.0f / std::sqrt((float)cfg->key_dim);
-  for (int i = 0; i < cfg->repeat_times; ++i) {        // vtd.py:350-412
+  const int i_lo = std::max(s_lo - 1, 0), i_hi = std::min(s_hi - 1, cfg->repeat_times);
+  for (int i = i_lo; i < i_hi; ++i) {                  // vtd.py:350-412
     const vtd_layer_weights& L = w->layers[i];
     if (fp8 && (L.ln1_colsum || L.ln2_colsum))
       return fail(VTD_ERR_UNSUPPORTED, "forward: LayerNorm fold (ln*_colsum) is not supported in VTD_FP8 mode");
@@ -552,6 +583,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
       kv = d.mlp_units[j];
     }
   }
+  if (!(s_lo <= n_stages - 1 && n_stages - 1 < s_hi)) return VTD_OK;
   // ---- mlp_head: Dense(17) + Reshape((17, -1)) as a scatter epilogue (vtd.py:454-463)
   {
     const size_t es = es_of(dt);
