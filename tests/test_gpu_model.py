@@ -230,3 +230,27 @@ def test_bf16_with_f32_residual_stream_env(cuda):
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
                        timeout=300, env=env, cwd=root)
     assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_load_weights_from_keras_hdf5(vtd, cuda, dtype):
+    """Model.load_weights('*.keras' / '*.h5'): the Keras 2.9 HDF5 layout of the reference's
+    model.save (vtd.py:2146, 2179) read by keras_h5 and run through vtd_forward, against the
+    fp64 oracle forward with the same weights (tests/golden/make_keras_h5.py: seed 3)."""
+    import shutil
+    import sys
+    import tempfile
+    sys.path.insert(0, GOLD)
+    from make_keras_h5 import SEED, TINY
+    w = V.init_weights(seed=SEED, **TINY)
+    x = V.synthetic_images(3, TINY["input_shape"], seed=11)
+    expect = V.forward(w, x, **TINY)
+    model = vtd.create_vision_transformer_detector(**TINY, dtype=dtype)
+    with tempfile.TemporaryDirectory() as d:           # the '.keras' spelling of the same file
+        p = os.path.join(d, "model.keras")
+        shutil.copy(os.path.join(GOLD, "tiny_keras.h5"), p)
+        model.load_weights(p)
+    for k, v in model.get_weight_dict().items():
+        assert np.array_equal(v, w[k]), k
+    ok, rel = within(model(torch.from_numpy(x).to(cuda)).cpu().numpy(), expect, TOL[dtype])
+    assert ok, f"{dtype}: max rel err {rel:.3e}"

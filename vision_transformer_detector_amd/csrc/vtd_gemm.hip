@@ -896,7 +896,11 @@ __device__ __forceinline__ void pp2_issue(char* smem, const PP2BufSrc& src, int 
                                              kt * 128, 0, 0);
 }
 
-template <bool TR, class Src>
+// DG (timing diagnostics only, wrong outputs): bit 0 = P0 skips its B reads (stale b0),
+// bit 1 = no DMA after the prologue, bit 2 = no LDS reads after the first K-tile,
+// bit 3 = every DMA re-fetches K-tile 0 (L2-resident source, same instruction count),
+// bit 4 = (schedule, correct) Y0(t+2) issued in P2 with X0(t+2) instead of in P3
+template <bool TR, class Src, int DG = 0>
 __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, const Src& src,
                                              int nk, int wave, int wm, int wn, int fr, int fg) {
   // prologue: tile 0 complete, tile 1's X0/Y0/Y1 in flight
@@ -916,14 +920,20 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
   if (wm == 1) pp_barrier();                 // stagger G1 by one barrier
   const int ra = wm * 64, rb = wn * 32;      // group rows of this wave's quads
   bf16x8 a[4][2], b0[2][2], b1[2][2];
+  if constexpr (DG != 0) {
+    pp_load_a(a, smem, ra, fr, fg);
+    pp_load_b(b0, smem + 2 * 16384, rb, fr, fg);
+    pp_load_b(b1, smem + 3 * 16384, rb, fr, fg);
+  }
   for (int kt = 0; kt < nk; ++kt) {
     const char* st = smem + (kt & 1) * BSTAGE;
-    const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+    const bool n1 = kt + 1 < nk && !(DG & 2), n2 = kt + 2 < nk && !(DG & 2);
+    constexpr bool RD = !(DG & 4);
     // ---- P0
-    pp_load_a(a, st + 0 * 16384, ra, fr, fg);
-    if constexpr (TR) pp_load_b_t(b0, st + 2 * 16384, rb, fr, fg);
-    else pp_load_b(b0, st + 2 * 16384, rb, fr, fg);
-    if (n1) pp2_issue<1>(smem, src, wave, kt + 1, (kt + 1) & 1);
+    if (RD) pp_load_a(a, st + 0 * 16384, ra, fr, fg);
+    if constexpr (TR) { if (RD && !(DG & 1)) pp_load_b_t(b0, st + 2 * 16384, rb, fr, fg); }
+    else if (RD && !(DG & 1)) pp_load_b(b0, st + 2 * 16384, rb, fr, fg);
+    if (n1) pp2_issue<1>(smem, src, wave, (DG & 8) ? 0 : kt + 1, (kt + 1) & 1);
     if (n1) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     pp_barrier();
@@ -931,8 +941,8 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
     else pp_mfma<0, 0>(acc, a, b0);
     pp_barrier();
     // ---- P1
-    if constexpr (TR) pp_load_b_t(b1, st + 3 * 16384, rb, fr, fg);
-    else pp_load_b(b1, st + 3 * 16384, rb, fr, fg);
+    if constexpr (TR) { if (RD) pp_load_b_t(b1, st + 3 * 16384, rb, fr, fg); }
+    else if (RD) pp_load_b(b1, st + 3 * 16384, rb, fr, fg);
     if (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     pp_barrier();
@@ -940,16 +950,19 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
     else pp_mfma<0, 2>(acc, a, b1);
     pp_barrier();
     // ---- P2
-    pp_load_a(a, st + 1 * 16384, ra, fr, fg);
-    if (n2) pp2_issue<0>(smem, src, wave, kt + 2, kt & 1);
+    if (RD) pp_load_a(a, st + 1 * 16384, ra, fr, fg);
+    if (n2) pp2_issue<0>(smem, src, wave, (DG & 8) ? 0 : kt + 2, kt & 1);
+    if constexpr ((DG & 16) != 0) {
+      if (n2) pp2_issue<2>(smem, src, wave, (DG & 8) ? 0 : kt + 2, kt & 1);
+    }
     pp_barrier();
     if constexpr (TR) pp_mfma_t<4, 2>(acc, a, b1);
     else pp_mfma<4, 2>(acc, a, b1);
     pp_barrier();
     // ---- P3
     if (n2) {
-      pp2_issue<2>(smem, src, wave, kt + 2, kt & 1);
-      pp2_issue<3>(smem, src, wave, kt + 2, kt & 1);
+      if constexpr ((DG & 16) == 0) pp2_issue<2>(smem, src, wave, (DG & 8) ? 0 : kt + 2, kt & 1);
+      pp2_issue<3>(smem, src, wave, (DG & 8) ? 0 : kt + 2, kt & 1);
       asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1065,7 +1078,7 @@ __device__ __forceinline__ void epilogue_direct_generic(const f32x4 (&acc)[8][4]
   }
 }
 
-template <int EPI, bool BUF = false, bool TR = false>
+template <int EPI, bool BUF = false, bool TR = false, int DG = 0>
 __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
     int M, int N, int K, const bf16_t* __restrict__ A, int lda,
     const bf16_t* __restrict__ Bt, int ldb, int tiles_m, int tiles_n, EpiArgs e) {
@@ -1099,7 +1112,7 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fg = lane >> 4;
-  pp2_mainloop<TR>(acc, smem, src, K / 64, wave, wm, wn, fr, fg);
+  pp2_mainloop<TR, Src, DG>(acc, smem, src, K / 64, wave, wm, wn, fr, fg);
   const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
   if constexpr (TR) {
     if constexpr (EPI != EPI_GENERIC) {
@@ -2002,6 +2015,28 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
       const bool pp2t = variant == 9 || (variant == 10 && e.act != VTD_ACT_NONE);
       const bool pp2b = variant == 8 || (variant == 10 && !pp2t);
       if (variant == 5) e.scatter_tokens = -2;      // diag: all tiles store to rows 0..255
+      // 21..27: main-loop timing diagnostics (pp2_mainloop DG = variant - 20; wrong outputs)
+      // on the plain bf16 epilogue; other epilogues run the default kernels
+      if (variant > 20 && variant < 37 && code == 4) {
+        static bool dattr = false;
+        const void* dfn[] = {
+#define VTD_DG_FN(D) reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<4, true, false, D>),
+            VTD_DG_FN(1) VTD_DG_FN(2) VTD_DG_FN(3) VTD_DG_FN(4) VTD_DG_FN(5) VTD_DG_FN(6) VTD_DG_FN(7)
+            VTD_DG_FN(8) VTD_DG_FN(9) VTD_DG_FN(10) VTD_DG_FN(11) VTD_DG_FN(12) VTD_DG_FN(13)
+            VTD_DG_FN(14) VTD_DG_FN(15) VTD_DG_FN(16)
+#undef VTD_DG_FN
+        };
+        if (!dattr) {
+          for (const void* f : dfn)
+            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
+          dattr = true;
+        }
+        void* args[] = {&M, &N, &K, (void*)&a16, &lda, (void*)&b16, &ldb,
+                        const_cast<int*>(&tiles_m), const_cast<int*>(&tiles_n), &e};
+        (void)hipLaunchKernel(dfn[variant - 21], g, b, args, 2 * BSTAGE, stream);
+        VTD_LAUNCH_CHECK("gemm");
+        return VTD_OK;
+      }
       const dim3 gp(std::min(tiles_m * tiles_n, num_cu));
       // pp3 (vtd_gemm_pp3.hip, persistent, one DMA pipeline across tiles): opt-in
       // variant 11.  Isolated it beats pp2 on long-K bf16 layers (mlp2 768 x 3072 -> 1536:

@@ -215,10 +215,16 @@ class Model:
             np.savez(path, **d)
 
     def load_weights(self, path: str) -> None:
-        """Read weights written by save_weights or by tools/keras_weights_to_npz.py from
-        a reference Keras model (names may carry TF's ':0' suffix).  Only loaders that
-        execute nothing from the file are used (np.load allow_pickle=False, safetensors)."""
-        if path.endswith(".safetensors"):
+        """Read weights from a Keras 2.x HDF5 file -- the reference's `model.save('*.keras')`
+        (vtd.py:2146, 2179; HDF5 under TF 2.9) or `save_weights('*.h5')` -- by Keras weight
+        name (keras_h5.read_keras_weights), or from files written by save_weights /
+        tools/keras_weights_to_npz.py (names may carry TF's ':0' suffix).  Only loaders
+        that execute nothing from the file are used (the HDF5 parser here, np.load
+        allow_pickle=False, safetensors)."""
+        if path.endswith((".keras", ".h5", ".hdf5")):
+            from .keras_h5 import read_keras_weights
+            raw, _ = read_keras_weights(path)
+        elif path.endswith(".safetensors"):
             from safetensors.numpy import load_file
             raw = load_file(path)
         else:
