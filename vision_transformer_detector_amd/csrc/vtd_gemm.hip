@@ -899,7 +899,9 @@ __device__ __forceinline__ void pp2_issue(char* smem, const PP2BufSrc& src, int 
 // DG (timing diagnostics only, wrong outputs): bit 0 = P0 skips its B reads (stale b0),
 // bit 1 = no DMA after the prologue, bit 2 = no LDS reads after the first K-tile,
 // bit 3 = every DMA re-fetches K-tile 0 (L2-resident source, same instruction count),
-// bit 4 = (schedule, correct) Y0(t+2) issued in P2 with X0(t+2) instead of in P3
+// bit 4 = (schedule, correct) Y0(t+2) issued in P2 with X0(t+2) instead of in P3,
+// bit 7 = the steady-state counted waits leave 8 more DMA instructions in flight (reads may
+// see unlanded data: a latency probe)
 template <bool TR, class Src, int DG = 0>
 __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, const Src& src,
                                              int nk, int wave, int wm, int wn, int fr, int fg) {
@@ -934,8 +936,12 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
     if constexpr (TR) { if (RD && !(DG & 1)) pp_load_b_t(b0, st + 2 * 16384, rb, fr, fg); }
     else if (RD && !(DG & 1)) pp_load_b(b0, st + 2 * 16384, rb, fr, fg);
     if (n1) pp2_issue<1>(smem, src, wave, (DG & 8) ? 0 : kt + 1, (kt + 1) & 1);
-    if (n1) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (n1) {
+      if constexpr ((DG & 128) != 0) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     pp_barrier();
     if constexpr (TR) pp_mfma_t<0, 0>(acc, a, b0);
     else pp_mfma<0, 0>(acc, a, b0);
@@ -943,8 +949,12 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
     // ---- P1
     if constexpr (TR) { if (RD) pp_load_b_t(b1, st + 3 * 16384, rb, fr, fg); }
     else if (RD) pp_load_b(b1, st + 3 * 16384, rb, fr, fg);
-    if (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (n1) {
+      if constexpr ((DG & 128) != 0) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     pp_barrier();
     if constexpr (TR) pp_mfma_t<0, 2>(acc, a, b1);
     else pp_mfma<0, 2>(acc, a, b1);
@@ -955,15 +965,18 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
     if constexpr ((DG & 16) != 0) {
       if (n2) pp2_issue<2>(smem, src, wave, (DG & 8) ? 0 : kt + 2, kt & 1);
     }
+
     pp_barrier();
     if constexpr (TR) pp_mfma_t<4, 2>(acc, a, b1);
     else pp_mfma<4, 2>(acc, a, b1);
     pp_barrier();
     // ---- P3
     if (n2) {
-      if constexpr ((DG & 16) == 0) pp2_issue<2>(smem, src, wave, (DG & 8) ? 0 : kt + 2, kt & 1);
+      if constexpr ((DG & 16) == 0)
+        pp2_issue<2>(smem, src, wave, (DG & 8) ? 0 : kt + 2, kt & 1);
       pp2_issue<3>(smem, src, wave, (DG & 8) ? 0 : kt + 2, kt & 1);
-      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      if constexpr ((DG & 128) != 0) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -2017,13 +2030,13 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
       if (variant == 5) e.scatter_tokens = -2;      // diag: all tiles store to rows 0..255
       // 21..27: main-loop timing diagnostics (pp2_mainloop DG = variant - 20; wrong outputs)
       // on the plain bf16 epilogue; other epilogues run the default kernels
-      if (variant > 20 && variant < 37 && code == 4) {
+      if (((variant > 20 && variant < 37) || variant == 40) && code == 4) {
         static bool dattr = false;
         const void* dfn[] = {
 #define VTD_DG_FN(D) reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<4, true, false, D>),
             VTD_DG_FN(1) VTD_DG_FN(2) VTD_DG_FN(3) VTD_DG_FN(4) VTD_DG_FN(5) VTD_DG_FN(6) VTD_DG_FN(7)
             VTD_DG_FN(8) VTD_DG_FN(9) VTD_DG_FN(10) VTD_DG_FN(11) VTD_DG_FN(12) VTD_DG_FN(13)
-            VTD_DG_FN(14) VTD_DG_FN(15) VTD_DG_FN(16)
+            VTD_DG_FN(14) VTD_DG_FN(15) VTD_DG_FN(16) VTD_DG_FN(128)
 #undef VTD_DG_FN
         };
         if (!dattr) {
@@ -2033,7 +2046,7 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
         }
         void* args[] = {&M, &N, &K, (void*)&a16, &lda, (void*)&b16, &ldb,
                         const_cast<int*>(&tiles_m), const_cast<int*>(&tiles_n), &e};
-        (void)hipLaunchKernel(dfn[variant - 21], g, b, args, 2 * BSTAGE, stream);
+        (void)hipLaunchKernel(dfn[variant == 40 ? 16 : variant - 21], g, b, args, 2 * BSTAGE, stream);
         VTD_LAUNCH_CHECK("gemm");
         return VTD_OK;
       }
