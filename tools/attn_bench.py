@@ -1,0 +1,55 @@
+"""Attention kernel micro-benchmark through the C-ABI at the C2 shape (B=256, N=196, 12
+heads x 64, bf16), for rocprofv3 PMC passes and variant A/B (VTD_ATTN_VARIANT).
+  python tools/attn_bench.py [--reps 20] [--B 256] [--N 196] [--flush]"""
+import argparse
+import json
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vision_transformer_detector_amd import _lib as L  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--B", type=int, default=256)
+    ap.add_argument("--N", type=int, default=196)
+    ap.add_argument("--H", type=int, default=12)
+    ap.add_argument("--flush", action="store_true", help="evict the MALL between reps")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    B, N, H, dkp = a.B, a.N, a.H, 64
+    ld = 3 * H * dkp
+    g = torch.Generator(device=dev).manual_seed(0)
+    qkv = (torch.randn(B * N, ld, generator=g, device=dev) * 1.5).to(torch.bfloat16)
+    out = torch.empty(B * N, H * dkp, device=dev, dtype=torch.bfloat16)
+    junk = torch.empty(512 << 20, dtype=torch.uint8, device=dev) if a.flush else None
+    st = L.stream_ptr()
+    call = lambda: L.check(L.lib.vtd_attention(qkv.data_ptr(), B, N, H, dkp, ld, 1 / math.sqrt(64),
+                                               out.data_ptr(), H * dkp, L.BF16, st))
+    for _ in range(3):
+        call()
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ms = 0.0
+    for _ in range(a.reps):
+        if junk is not None:
+            junk.fill_(1)
+        t0.record()
+        call()
+        t1.record()
+        torch.cuda.synchronize()
+        ms += t0.elapsed_time(t1)
+    us = 1e3 * ms / a.reps
+    byts = B * N * (ld + H * dkp) * 2
+    print(json.dumps({"variant": os.environ.get("VTD_ATTN_VARIANT", "default"), "B": B, "N": N,
+                      "flush": a.flush, "us": round(us, 2),
+                      "hbm_tbs": round(byts / us / 1e6, 2),
+                      "tflops": round(4.0 * B * H * N * N * 64 / us / 1e6, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -55,6 +55,37 @@ def run(name, spec, reps, dev):
     torch.cuda.synchronize()
     ms = t0.elapsed_time(t1) / reps
     res = {"shape": name, "us": round(ms * 1e3, 1), "tflops": round(2 * M * N * K / ms / 1e9, 1)}
+    if os.environ.get("VTD_GEMM_SPLIT2"):
+        # the same problem as two M-halves on two streams at once (the forward's two-stream
+        # micro-batching), and the two halves back to back on one stream
+        h = (M // 2 // 256) * 256
+        s1, s2 = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+        e1, e2 = L.VtdEpilogue(), L.VtdEpilogue()
+        for ee, r0 in ((e1, 0), (e2, h)):
+            ee.bias, ee.act, ee.ldo, ee.out_dtype = e.bias, e.act, N, e.out_dtype
+            ee.out = out.data_ptr() + r0 * N * out.element_size()
+            if res:
+                ee.resid, ee.ldr = ee.out, N
+
+        def halves(st_a, st_b):
+            for ee, r0, mm, stv in ((e1, 0, h, st_a), (e2, h, M - h, st_b)):
+                L.check(L.lib.vtd_gemm(mm, N, K, A.data_ptr() + r0 * K * 2, K, Bt.data_ptr(), K,
+                                       L.BF16, ctypes.byref(ee), stv.cuda_stream))
+        cur = torch.cuda.current_stream()
+        for label, (sa, sb) in (("two_streams", (s1, s2)), ("one_stream", (s1, s1))):
+            for _ in range(3):
+                halves(sa, sb)
+            torch.cuda.synchronize()
+            t0.record(cur)
+            s1.wait_stream(cur)
+            s2.wait_stream(cur)
+            for _ in range(reps):
+                halves(sa, sb)
+            cur.wait_stream(s1)
+            cur.wait_stream(s2)
+            t1.record(cur)
+            torch.cuda.synchronize()
+            res["halves_" + label + "_us"] = round(t0.elapsed_time(t1) / reps * 1e3, 1)
     if os.environ.get("VTD_GEMM_REF_LIB"):
         # vendor-library reference (torch.matmul -> hipBLASLt), timing comparison only
         Bk = Bt.t()

@@ -1907,13 +1907,23 @@ int gemm_variant() {
   return variant;
 }
 
+// Fewest 256 x 256 tiles for which the bf16 path takes the 256-tile kernels (below: the
+// 128 x 128 gemm_tn_kernel).  VTD_PP2_MIN_TILES overrides (A/B of the head's small GEMMs).
+int pp2_min_tiles() {
+  static const int t = [] {
+    const char* v = getenv("VTD_PP2_MIN_TILES");
+    return v ? std::max(1, atoi(v)) : 128;
+  }();
+  return t;
+}
+
 // Whether vtd_gemm can emit the partial LayerNorm statistics (epilogue.statout) for this
 // problem: every tile full and on the pp2b / pp2t fast epilogues with a bf16 output.
 bool gemm_emits_stats(int M, int N, int dtype, const vtd_epilogue* e) {
   const int tiles = ((M + BBM - 1) / BBM) * ((N + BBN - 1) / BBN);
   const int v = gemm_variant();
   auto a16 = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
-  return dtype == VTD_BF16 && e->out_dtype == VTD_BF16 && tiles >= 128 && N > 64 &&
+  return dtype == VTD_BF16 && e->out_dtype == VTD_BF16 && tiles >= pp2_min_tiles() && N > 64 &&
          M % BBM == 0 && N % BBN == 0 && (v == 8 || v == 9 || v == 10) && e->bias &&
          e->scatter_tokens <= 0 && e->ldo % 8 == 0 && a16(e->out) && a16(e->bias) &&
          (!e->resid || (e->ldr % 8 == 0 && a16(e->resid))) &&
@@ -1960,7 +1970,7 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
   ProfScope ps(stream, PROF_GEMM, flops > 0 ? flops : 2.0 * M * N * (double)K);
   const int tiles_m = (M + BBM - 1) / BBM, tiles_n = (N + BBN - 1) / BBN;
   // N <= 64 (the Dense(17) head projection): 128 x 128 tiles waste 8x less MFMA work
-  if (dtype == VTD_BF16 && tiles_m * tiles_n >= 128 && N > 64) {
+  if (dtype == VTD_BF16 && tiles_m * tiles_n >= pp2_min_tiles() && N > 64) {
     static bool attr = false;
     if (!attr) {
       const void* fns[] = {

@@ -216,16 +216,25 @@ Plan make_plan(const vtd_config* c, const vtd_dims& d) {
 // instead of leaving CUs idle.  VTD_STREAMS=1 disables it; so does per-kernel profiling
 // (vtd_profile_enable): each profiled launch then runs alone and its events time it.
 constexpr int kMaxSplit = 4;   // VTD_STREAMS is clamped to [1, kMaxSplit]
-int split_count(const vtd_config* c, const vtd_dims& d) {
-  if (prof().enabled) return 1;
+// fewest 256-row tiles per part (VTD_SPLIT_MIN_TILES; C2 at B = 256, 2 parts: 98 each)
+int split_min_tiles() {
+  static const int t = [] {
+    const char* v = getenv("VTD_SPLIT_MIN_TILES");
+    return v ? std::max(1, atoi(v)) : 48;
+  }();
+  return t;
+}
+int split_parts(const vtd_config* c, const vtd_dims& d) {
   static const int streams = [] {
     const char* v = getenv("VTD_STREAMS");
     return v ? atoi(v) : 2;
   }();
-  // only where each part still has >= 48 row tiles of 256 (C2 at B = 256, 2 parts: 98 each)
   int ns = std::min(std::max(streams, 1), (int)kMaxSplit);
-  while (ns > 1 && (c->batch < ns || d.rows < (int64_t)ns * 48 * 256)) --ns;
+  while (ns > 1 && (c->batch < ns || d.rows < (int64_t)ns * split_min_tiles() * 256)) --ns;
   return ns;
+}
+int split_count(const vtd_config* c, const vtd_dims& d) {
+  return prof().enabled ? 1 : split_parts(c, d);
 }
 vtd_config sub_config(const vtd_config* c, int part, int nsplit) {
   vtd_config s = *c;
@@ -236,14 +245,9 @@ vtd_config sub_config(const vtd_config* c, int part, int nsplit) {
 // workspace of either form (profiling can toggle between them)
 size_t split_workspace(const vtd_config* c, const vtd_dims& d) {
   const size_t whole = make_plan(c, d).total;
-  static const int streams = [] {
-    const char* v = getenv("VTD_STREAMS");
-    return v ? atoi(v) : 2;
-  }();
   vtd_dims dd;
   if (derive(c, &dd) != VTD_OK) return 0;
-  int ns = std::min(std::max(streams, 1), (int)kMaxSplit);
-  while (ns > 1 && (c->batch < ns || dd.rows < (int64_t)ns * 48 * 256)) --ns;
+  const int ns = split_parts(c, dd);
   if (ns == 1) return whole;
   size_t total = 0;
   for (int i = 0; i < ns; ++i) {

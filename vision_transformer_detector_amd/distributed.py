@@ -48,6 +48,19 @@ def broadcast_weights(model, src: int = 0, group=None) -> None:
     model.set_weights(out)
 
 
+def gather_padded(padded: torch.Tensor, group=None) -> torch.Tensor:
+    """The collective: every rank's equally sized `padded` shard, concatenated in rank
+    order (one all_gather_into_tensor on RCCL; a list all_gather on gloo)."""
+    world = dist.get_world_size(group)
+    out = torch.empty((world * padded.shape[0],) + tuple(padded.shape[1:]), dtype=padded.dtype,
+                      device=padded.device)
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, padded.contiguous(), group=group)
+    else:
+        dist.all_gather(list(out.chunk(world)), padded.contiguous(), group=group)
+    return out
+
+
 def all_gather_detections(local: torch.Tensor, global_batch: int, group=None) -> torch.Tensor:
     """Gather every rank's (b_r, 17, 6) fp32 shard into (global_batch, 17, 6) in rank
     order.  Shards are padded to the largest shard so one fixed-size collective suffices
@@ -66,12 +79,7 @@ def all_gather_detections(local: torch.Tensor, global_batch: int, group=None) ->
         padded = torch.zeros((ms,) + tuple(local.shape[1:]), dtype=local.dtype,
                              device=local.device)
         padded[:local.shape[0]] = local
-    out = torch.empty((world * ms,) + tuple(local.shape[1:]), dtype=local.dtype,
-                      device=local.device)
-    if dist.get_backend(group) == "nccl":
-        dist.all_gather_into_tensor(out, padded.contiguous(), group=group)
-    else:
-        dist.all_gather(list(out.chunk(world)), padded.contiguous(), group=group)
+    out = gather_padded(padded, group)
     pieces = [out[r * ms: r * ms + (shard_bounds(global_batch, r, world)[1] -
                                    shard_bounds(global_batch, r, world)[0])]
               for r in range(world)]
