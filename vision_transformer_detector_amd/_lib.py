@@ -12,7 +12,9 @@ import os
 
 import torch  # noqa: F401  (must precede loading libvtd.so, see module doc)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvtd.so")
+# VTD_LIB_PATH: an alternative build of the same sources (A/B experiments of build-time knobs)
+LIB_PATH = os.environ.get("VTD_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                          "libvtd.so")
 
 ABI_VERSION = 9
 KALIGN = 64

@@ -885,6 +885,13 @@ __device__ __forceinline__ void pp2b_sources(PP2BufSrc& s, const bf16_t* A, int 
     }
 }
 
+// cache policy of the operand DMA (buffer aux bits: 1 sc0, 2 nt, 16 sc1); build-time A/B knob
+#ifndef VTD_A_LOAD_AUX
+#define VTD_A_LOAD_AUX 0
+#endif
+#ifndef VTD_B_LOAD_AUX
+#define VTD_B_LOAD_AUX 0
+#endif
 template <int G>
 __device__ __forceinline__ void pp2_issue(char* smem, const PP2BufSrc& src, int wave, int kt,
                                           int stage) {
@@ -893,7 +900,7 @@ __device__ __forceinline__ void pp2_issue(char* smem, const PP2BufSrc& src, int 
   for (int j = 0; j < 2; ++j)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(G < 2 ? src.ra : src.rb,
                                              (lds_void_t*)(dst + j * 1024), 16, src.off[G][j],
-                                             kt * 128, 0, 0);
+                                             kt * 128, 0, G < 2 ? VTD_A_LOAD_AUX : VTD_B_LOAD_AUX);
 }
 
 // DG (timing diagnostics only, wrong outputs): bit 0 = P0 skips its B reads (stale b0),

@@ -412,7 +412,13 @@ bool gemm_pp3_launch(int M, int N, int K, const bf16_t* A, int lda, const bf16_t
   if (epi->resid && epi->out_dtype != VTD_F32) return false;   // f32 residual only
   const int tiles_m = (M + BBM - 1) / BBM, tiles_n = (N + BBN - 1) / BBN;
   const P3Epi e{epi->bias, static_cast<const float*>(epi->resid), epi->ldr, epi->out, epi->ldo};
-  const dim3 grid(std::min(tiles_m * tiles_n, num_cu)), block(BNT);
+  // VTD_PP3_GRID: persistent blocks per launch (default one per CU); a smaller grid leaves
+  // CUs to a kernel running concurrently on another stream
+  static const int grid_cap = [] {
+    const char* v = getenv("VTD_PP3_GRID");
+    return v ? std::max(1, atoi(v)) : 1 << 30;
+  }();
+  const dim3 grid(std::min({tiles_m * tiles_n, num_cu, grid_cap})), block(BNT);
   static bool attr = false;
   if (!attr) {
 #define VTD_P3_FN(C) reinterpret_cast<const void*>(&gemm_tn_bf16_pp3_kernel<C>),
