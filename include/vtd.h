@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define VTD_ABI_VERSION 9
+#define VTD_ABI_VERSION 10
 #define VTD_KALIGN 64          /* K / row padding granule, elements              */
 #define VTD_MAX_MLP 16         /* max encoder_mlp_quantities                     */
 #define VTD_MAX_HEAD 64        /* max mlp_head layers * repeats                   */
@@ -284,6 +284,23 @@ int vtd_decode_detections(const float* logits_dev, int64_t n, float* dets_dev,
 int vtd_resize_with_pad(const uint8_t* pixels_dev, const int64_t* offsets_dev,
                         const int32_t* sizes_dev, int B, int target_h, int target_w,
                         float* out_dev, void* stream);
+
+/* JPEG decode on the device, tf.image.decode_image(file, channels=3)
+ * (vision_transformer_utilities.py:431) for baseline JPEG: sequential Huffman, 8-bit, 1 or 3
+ * components, 4:4:4 / 4:2:2 / 4:2:0, restart intervals.  libjpeg-turbo's decode path (what TF
+ * uses): ISLOW IDCT, fancy upsampling, YCbCr -> RGB; gray -> RGB replicated.  Other JPEGs
+ * (progressive, CMYK, 12-bit, ...) return VTD_ERR_UNSUPPORTED with the reason.
+ * vtd_jpeg_info: header only (host).  The images are HOST buffers; their marker segments are
+ * parsed on the host, the entropy-coded data + derived tables copied to the workspace on
+ * `stream` (through a pinned staging buffer the library reuses), image i written as RGB
+ * uint8 HWC at out_dev + out_offsets[i] (host array). */
+int vtd_jpeg_info(const uint8_t* jpeg, size_t len, int* h, int* w, int* comps);
+int vtd_jpeg_workspace_bytes(const uint8_t* const* jpegs, const size_t* lens, int n,
+                             int32_t* dims /* nullable: 2n ints, (h, w) per image */,
+                             size_t* bytes);
+int vtd_jpeg_decode(const uint8_t* const* jpegs, const size_t* lens, int n, uint8_t* out_dev,
+                    const int64_t* out_offsets, void* workspace_dev, size_t workspace_bytes,
+                    void* stream);
 
 /* ---------------------------------------------------------------- forward ------ */
 /* model(images, training=False) (vtd.py:579-581, ipynb:836):

@@ -1,10 +1,11 @@
 """Input pipeline image transform on the device.
 
-Mirrors `_get_image_tensor_coco` (`vision_transformer_utilities.py:418-449`) for a batch of
-already decoded images: `tf.image.resize_with_pad` to the model size (bilinear, half-pixel
-centers), `clip_by_value(0, 255)`, `/ 127.5 - 1`, written as one NHWC fp32 batch that
-`Model.__call__` takes directly. One `vtd_resize_with_pad` launch per batch; file reading and
-JPEG/PNG decode (`tf.io.read_file` / `tf.image.decode_image`) stay with the caller.
+Mirrors `_get_image_tensor_coco` (`vision_transformer_utilities.py:418-449`) for a batch:
+`tf.image.decode_image(file, channels=3)` for JPEG files (`decode_jpegs`: libjpeg-turbo's
+baseline decode path on the device, vtd_jpeg_decode), then `tf.image.resize_with_pad` to the
+model size (bilinear, half-pixel centers), `clip_by_value(0, 255)`, `/ 127.5 - 1`, written as
+one NHWC fp32 batch that `Model.__call__` takes directly (one `vtd_resize_with_pad` launch).
+File reading stays with the caller (`get_image_tensors_from_files` reads the bytes).
 """
 from __future__ import annotations
 
@@ -58,6 +59,71 @@ def get_image_tensors(images, target_height: int = MODEL_IMAGE_HEIGHT,
     out = torch.empty(len(flats), target_height, target_width, 3, dtype=torch.float32, device=dev)
     with torch.cuda.device(dev):
         L.check(L.lib.vtd_resize_with_pad(L.ptr(pixels), L.ptr(offs), L.ptr(szs), len(flats),
+                                          target_height, target_width, L.ptr(out),
+                                          L.stream_ptr(stream)), "resize_with_pad")
+    return out, sizes
+
+
+def decode_jpegs(files, device="cuda", stream=None):
+    """JPEG file bytes (a list of `bytes`) -> (packed RGB uint8 pixels on `device`, per-image
+    byte offsets (int64, host), [(height, width), ...]): `tf.image.decode_image(f, channels=3)`
+    (vision_transformer_utilities.py:431) for baseline JPEGs, decoded on the device by
+    vtd_jpeg_decode.  Unsupported JPEG flavours (progressive, CMYK, 12-bit) raise
+    ValueError naming the reason; nothing falls back to a host decoder."""
+    import ctypes
+    if len(files) == 0:
+        raise ValueError("decode_jpegs: empty file list")
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise ValueError(f"decode_jpegs runs on a HIP device, got {dev}")
+    files = [bytes(f) for f in files]      # c_char_p points into each bytes object: no copy
+    n = len(files)
+    ptrs = (ctypes.c_char_p * n)(*files)
+    lens = (ctypes.c_size_t * n)(*[len(f) for f in files])
+    dims = np.zeros((n, 2), np.int32)
+    ws_bytes = ctypes.c_size_t()
+    rc = L.lib.vtd_jpeg_workspace_bytes(ptrs, lens, n, dims.ctypes.data, ctypes.byref(ws_bytes))
+    if rc != 0:
+        raise ValueError(L.lib.vtd_last_error().decode())
+    sizes = [(int(h), int(w)) for h, w in dims]
+    offsets = np.zeros(n, np.int64)
+    offsets[1:] = np.cumsum(dims[:, 0].astype(np.int64) * dims[:, 1] * 3)[:-1]
+    total = int(offsets[-1]) + sizes[-1][0] * sizes[-1][1] * 3
+    pixels = torch.empty(total, dtype=torch.uint8, device=dev)
+    ws = torch.empty(int(ws_bytes.value), dtype=torch.uint8, device=dev)
+    offs = (ctypes.c_int64 * n)(*offsets.tolist())
+    with torch.cuda.device(dev):
+        L.check(L.lib.vtd_jpeg_decode(ptrs, lens, n, L.ptr(pixels), offs, L.ptr(ws),
+                                      ws_bytes.value, L.stream_ptr(stream)), "jpeg_decode")
+    if stream is not None:                 # the allocator must not recycle the workspace
+        ws.record_stream(stream)           # before the kernels on `stream` have run
+    return pixels, offsets, sizes
+
+
+def get_image_tensors_from_files(paths_or_bytes, target_height: int = MODEL_IMAGE_HEIGHT,
+                                 target_width: int = MODEL_IMAGE_WIDTH, device="cuda",
+                                 stream=None):
+    """`_get_image_tensor_coco` for a batch of JPEG files (paths or bytes): read, decode on
+    the device (decode_jpegs), resize_with_pad / clip / normalise on the device ->
+    (images (B, target_height, target_width, 3) fp32 in [-1, 1], original sizes)."""
+    files = []
+    for p in paths_or_bytes:
+        if isinstance(p, (bytes, bytearray, memoryview)):
+            files.append(bytes(p))
+        else:
+            with open(p, "rb") as f:
+                files.append(f.read())
+    pixels, offsets, sizes = decode_jpegs(files, device=device, stream=stream)
+    dev = torch.device(device)
+    for h, w in sizes:
+        if not _resized_side_positive(h, w, target_height, target_width):
+            raise ValueError(f"image {h}x{w} cannot be resized with pad to "
+                             f"{target_height}x{target_width} (a resized side would be 0)")
+    offs = torch.from_numpy(offsets).to(dev)
+    szs = torch.tensor(sizes, dtype=torch.int32).to(dev)
+    out = torch.empty(len(files), target_height, target_width, 3, dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        L.check(L.lib.vtd_resize_with_pad(L.ptr(pixels), L.ptr(offs), L.ptr(szs), len(files),
                                           target_height, target_width, L.ptr(out),
                                           L.stream_ptr(stream)), "resize_with_pad")
     return out, sizes
