@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstring>
 #include <initializer_list>
+#include <vector>
 
 #include "vtd.h"
 
@@ -30,6 +31,35 @@ static vtd_config preset(int b, int hw, int p, int d, int heads, int kd, int q, 
   c.use_mish = mish; c.dtype = dtype;
   return c;
 }
+
+// 11x9 4:2:0 baseline JPEG with a restart marker per MCU row (Pillow, quality 70)
+static const uint8_t kJpeg[] = {
+    255,216,255,224,0,16,74,70,73,70,0,1,1,0,0,1,0,1,0,0,255,219,0,67,0,10,7,7,8,7,6,10,8,8,8,11,10,
+    10,11,14,24,16,14,13,13,14,29,21,22,17,24,35,31,37,36,34,31,34,33,38,43,55,47,38,41,52,41,33,34,
+    48,65,49,52,57,59,62,62,62,37,46,68,73,67,60,72,55,61,62,59,255,219,0,67,1,10,11,11,14,13,14,28,
+    16,16,28,59,40,34,40,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,
+    59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,255,192,0,17,8,0,9,0,
+    11,3,1,34,0,2,17,1,3,17,1,255,196,0,31,0,0,1,5,1,1,1,1,1,1,0,0,0,0,0,0,0,0,1,2,3,4,5,6,7,8,9,10,
+    11,255,196,0,181,16,0,2,1,3,3,2,4,3,5,5,4,4,0,0,1,125,1,2,3,0,4,17,5,18,33,49,65,6,19,81,97,7,
+    34,113,20,50,129,145,161,8,35,66,177,193,21,82,209,240,36,51,98,114,130,9,10,22,23,24,25,26,37,
+    38,39,40,41,42,52,53,54,55,56,57,58,67,68,69,70,71,72,73,74,83,84,85,86,87,88,89,90,99,100,101,
+    102,103,104,105,106,115,116,117,118,119,120,121,122,131,132,133,134,135,136,137,138,146,147,148,
+    149,150,151,152,153,154,162,163,164,165,166,167,168,169,170,178,179,180,181,182,183,184,185,186,
+    194,195,196,197,198,199,200,201,202,210,211,212,213,214,215,216,217,218,225,226,227,228,229,230,
+    231,232,233,234,241,242,243,244,245,246,247,248,249,250,255,196,0,31,1,0,3,1,1,1,1,1,1,1,1,1,0,
+    0,0,0,0,0,1,2,3,4,5,6,7,8,9,10,11,255,196,0,181,17,0,2,1,2,4,4,3,4,7,5,4,4,0,1,2,119,0,1,2,3,17,
+    4,5,33,49,6,18,65,81,7,97,113,19,34,50,129,8,20,66,145,161,177,193,9,35,51,82,240,21,98,114,209,
+    10,22,36,52,225,37,241,23,24,25,26,38,39,40,41,42,53,54,55,56,57,58,67,68,69,70,71,72,73,74,83,
+    84,85,86,87,88,89,90,99,100,101,102,103,104,105,106,115,116,117,118,119,120,121,122,130,131,132,
+    133,134,135,136,137,138,146,147,148,149,150,151,152,153,154,162,163,164,165,166,167,168,169,170,
+    178,179,180,181,182,183,184,185,186,194,195,196,197,198,199,200,201,202,210,211,212,213,214,215,
+    216,217,218,226,227,228,229,230,231,232,233,234,242,243,244,245,246,247,248,249,250,255,221,0,4,
+    0,1,255,218,0,12,3,1,0,2,17,3,17,0,63,0,98,249,254,96,158,230,105,110,74,225,90,99,188,182,240,
+    221,0,7,104,201,10,121,227,228,192,60,102,157,107,13,147,91,169,26,108,243,0,72,14,176,121,128,
+    128,72,24,96,192,17,142,42,150,173,255,0,30,86,191,245,210,111,253,1,171,182,111,245,211,127,
+    215,105,63,244,35,90,58,50,115,81,82,105,187,187,166,214,214,236,250,223,240,243,211,151,25,82,
+    157,40,65,168,104,210,118,245,87,234,158,218,253,231,255,217,
+};
 
 int main() {
   CHECK(vtd_abi_version() == VTD_ABI_VERSION);
@@ -91,6 +121,26 @@ int main() {
   CHECK(vtd_forward(&cases[1].c, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr) ==
         VTD_ERR_INVALID_ARG);
   CHECK(vtd_decode(nullptr, 17, nullptr, nullptr) == VTD_ERR_INVALID_ARG);
+  // JPEG host side: header walk, planning, every truncation and a corrupted copy (host only)
+  {
+    int h = 0, w = 0, c = 0;
+    CHECK(vtd_jpeg_info(kJpeg, sizeof(kJpeg), &h, &w, &c) == VTD_OK);
+    CHECK(h == 9 && w == 11 && c == 3);
+    const uint8_t* ptrs[2] = {kJpeg, kJpeg};
+    size_t lens[2] = {sizeof(kJpeg), sizeof(kJpeg)};
+    int32_t dims[4] = {0, 0, 0, 0};
+    size_t bytes = 0;
+    CHECK(vtd_jpeg_workspace_bytes(ptrs, lens, 2, dims, &bytes) == VTD_OK);
+    CHECK(dims[0] == 9 && dims[1] == 11 && dims[2] == 9 && dims[3] == 11 && bytes > 0);
+    for (size_t cut = 0; cut < sizeof(kJpeg); ++cut) {
+      std::vector<uint8_t> part(kJpeg, kJpeg + cut);
+      (void)vtd_jpeg_info(part.data(), part.size(), &h, &w, &c);
+    }
+    std::vector<uint8_t> bad(kJpeg, kJpeg + sizeof(kJpeg));
+    for (size_t i = 2; i < bad.size(); i += 3) bad[i] ^= 0x5A;
+    (void)vtd_jpeg_info(bad.data(), bad.size(), &h, &w, &c);
+    CHECK(vtd_jpeg_info(nullptr, 10, &h, &w, &c) == VTD_ERR_INVALID_ARG);
+  }
   // profiling state (host only)
   CHECK(vtd_profile_reset() == VTD_OK);
   double ms[8];

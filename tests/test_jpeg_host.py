@@ -1,0 +1,110 @@
+"""CPU tests of the JPEG decoder's host side (vtd_jpeg_info / vtd_jpeg_workspace_bytes: the
+marker walk that feeds the device decoder; no GPU calls): image sizes agree with Pillow's
+header parse over the supported flavours, unsupported flavours come back as
+VTD_ERR_UNSUPPORTED naming the reason, and malformed input fails cleanly."""
+import ctypes
+import io
+
+import numpy as np
+import pytest
+from PIL import Image
+
+
+@pytest.fixture(scope="module")
+def L():
+    from vision_transformer_detector_amd import _lib
+    return _lib
+
+
+def _jpeg(h, w, mode="RGB", **kw):
+    rng = np.random.default_rng(h * 1000 + w)
+    img = Image.fromarray(rng.integers(0, 256, (h, w, 3), dtype=np.uint8)).convert(mode)
+    b = io.BytesIO()
+    img.save(b, format="JPEG", **kw)
+    return b.getvalue()
+
+
+def _plan(L, files):
+    n = len(files)
+    ptrs = (ctypes.c_char_p * n)(*files)
+    lens = (ctypes.c_size_t * n)(*[len(f) for f in files])
+    dims = np.zeros((n, 2), np.int32)
+    ws = ctypes.c_size_t()
+    rc = L.lib.vtd_jpeg_workspace_bytes(ptrs, lens, n, dims.ctypes.data, ctypes.byref(ws))
+    return rc, dims, ws.value
+
+
+def _info(L, f):
+    h, w, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    rc = L.lib.vtd_jpeg_info(f, len(f), ctypes.byref(h), ctypes.byref(w), ctypes.byref(c))
+    return rc, (h.value, w.value, c.value)
+
+
+SUPPORTED = [
+    (480, 640, "RGB", dict(quality=85, subsampling=2)),
+    (37, 53, "RGB", dict(quality=90, subsampling=0)),
+    (17, 4, "RGB", dict(quality=60, subsampling=1)),
+    (1, 1, "RGB", dict(quality=80)),
+    (33, 70, "L", dict(quality=50)),
+    (96, 80, "RGB", dict(quality=85, optimize=True)),
+    (72, 88, "RGB", dict(quality=85, restart_marker_rows=2)),
+]
+
+
+@pytest.mark.parametrize("h,w,mode,kw", SUPPORTED)
+def test_info_matches_pillow_header(L, h, w, mode, kw):
+    try:
+        f = _jpeg(h, w, mode, **kw)
+    except TypeError:
+        pytest.skip("this Pillow lacks an encoder option")
+    rc, (hh, ww, c) = _info(L, f)
+    assert rc == 0, L.lib.vtd_last_error()
+    im = Image.open(io.BytesIO(f))
+    assert (hh, ww) == (im.height, im.width)
+    assert c == (1 if mode == "L" else 3)
+
+
+def test_workspace_plan_dims_and_growth(L):
+    files = [_jpeg(h, w, m, **kw) for h, w, m, kw in SUPPORTED if "restart_marker_rows" not in kw]
+    rc, dims, ws = _plan(L, files)
+    assert rc == 0
+    assert [tuple(d) for d in dims] == [(h, w) for h, w, m, kw in SUPPORTED
+                                        if "restart_marker_rows" not in kw]
+    # the workspace holds at least the coefficients (2 B each) of every image's blocks
+    assert ws >= sum(((h + 15) // 16) * ((w + 15) // 16) * 6 * 128 for h, w in dims) // 2
+    rc2, _, ws2 = _plan(L, files + files)
+    assert rc2 == 0 and ws2 > ws
+
+
+def test_unsupported_flavours_name_the_reason(L):
+    prog = _jpeg(40, 40, quality=80, progressive=True)
+    rc, _ = _info(L, prog)
+    assert rc != 0 and b"progressive" in L.lib.vtd_last_error()
+    cmyk = _jpeg(16, 16, "CMYK", quality=80)
+    rc, _ = _info(L, cmyk)
+    assert rc != 0 and b"component" in L.lib.vtd_last_error()
+    rc, _, _ = _plan(L, [_jpeg(8, 8), prog])
+    assert rc != 0 and b"image 1" in L.lib.vtd_last_error()
+
+
+@pytest.mark.parametrize("data", [b"", b"\x00\x01not a jpeg", b"\xff\xd8", b"\xff\xd8\xff\xd9",
+                                  b"\xff\xd8\xff\xdb\x00\x43\x00"])
+def test_malformed_input_fails_cleanly(L, data):
+    if not data:
+        rc = L.lib.vtd_jpeg_info(b"\0", 0, None, None, None)
+    else:
+        rc, _ = _info(L, data)
+    assert rc != 0 and L.lib.vtd_last_error()
+
+
+def test_truncations_of_a_valid_file_never_crash(L):
+    f = _jpeg(24, 24, quality=75)
+    for cut in range(1, len(f), 7):
+        rc, _ = _info(L, f[:cut])        # a header cut short fails; a cut scan still parses
+        assert rc in (0,) or L.lib.vtd_last_error()
+
+
+def test_decode_requires_a_hip_device():
+    from vision_transformer_detector_amd.preprocess import decode_jpegs
+    with pytest.raises(ValueError, match="HIP device"):
+        decode_jpegs([_jpeg(8, 8)], device="cpu")
