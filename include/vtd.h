@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define VTD_ABI_VERSION 10
+#define VTD_ABI_VERSION 11
 #define VTD_KALIGN 64          /* K / row padding granule, elements              */
 #define VTD_MAX_MLP 16         /* max encoder_mlp_quantities                     */
 #define VTD_MAX_HEAD 64        /* max mlp_head layers * repeats                   */
@@ -187,6 +187,11 @@ typedef struct vtd_epilogue {
    * vtd_quantize_mx8 makes of the bf16-rounded output: e4m3 out[m * ldo + n] and
    * scale_out[n/128][scale_rows][4]. */
   uint8_t* scale_out; int64_t scale_rows;
+  /* transform_predictions (vtd.py:586-647) fused into the final Dense(6) (SURVEY §8b
+   * vtd_head_decode): with N == 6, an fp32 output and no scatter, detections[m * 6 + n] =
+   * sigmoid(C[m][n]), clipped to [0, 1] for n >= 2, times (1, 79, 608, 608, 608, 608) --
+   * what vtd_decode computes from the stored logits, bit for bit.  NULL: none. */
+  float* detections;
 } vtd_epilogue;
 int vtd_gemm(int M, int N, int K, const void* A_dev, int lda, const void* Bt_dev,
              int ldb, int dtype, const vtd_epilogue* epi, void* stream);

@@ -56,6 +56,22 @@ def test_tiny_golden(vtd, cuda, name, dtype):
 
 
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16", "float8"])
+@pytest.mark.parametrize("batch", [1, 5])
+def test_fused_decode_equals_transform_predictions(vtd, cuda, dtype, batch):
+    """transform_predictions fused into the final Dense(6) epilogue (vtd_epilogue.detections,
+    SURVEY §8b vtd_head_decode) gives the bits vtd_decode computes from the stored logits."""
+    kw, w, x, _, _ = load_tiny("tiny_gelu")
+    model = vtd.create_vision_transformer_detector(**kw, dtype=dtype)
+    model.set_weights(w)
+    xb = torch.from_numpy(np.concatenate([x] * batch)).to(cuda)
+    y, d = model.detect(xb)
+    ref = vtd.transform_predictions(y)
+    torch.cuda.synchronize()
+    assert d.shape == ref.shape == (x.shape[0] * batch, 17, 6)
+    assert torch.equal(d, ref)
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16", "float8"])
 @pytest.mark.parametrize("case", ["c1_default_b1", "c2_vitb16_b1", "c3_vitb16_640_b1",
                                   "c5_vitl16_384_b1"])
 def test_seeded_full_config(vtd, cuda, case, dtype):

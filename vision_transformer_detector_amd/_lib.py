@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must precede loading libvtd.so, see module doc)
 LIB_PATH = os.environ.get("VTD_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                           "libvtd.so")
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 KALIGN = 64
 MAX_MLP = 16
 MAX_HEAD = 64
@@ -76,7 +76,7 @@ class VtdEpilogue(ctypes.Structure):
         ("out", c_void_p), ("ldo", c_int), ("out_dtype", c_int), ("out2", c_void_p),
         ("ldo2", c_int), ("scatter_tokens", c_int), ("lnstat", c_void_p), ("colsum", c_void_p),
         ("statout", c_void_p), ("stat_ld", c_int), ("scale_out", c_void_p),
-        ("scale_rows", c_int64)]
+        ("scale_rows", c_int64), ("detections", c_void_p)]
 
 
 # name -> (restype, argtypes)

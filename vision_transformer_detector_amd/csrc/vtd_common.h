@@ -93,6 +93,16 @@ __device__ __forceinline__ uint32_t mx8_pack4(float a, float b, float c, float d
   w = __builtin_amdgcn_cvt_pk_fp8_f32(c * inv, d * inv, w, true);
   return (uint32_t)w;
 }
+// transform_predictions (vtd.py:586-647) of logit v in column f of the (.., 6) output:
+// sigmoid; clip the last 4 to [0, 1]; [conf, cls * (CLASSES-1), cx * W, cy * H, h * H, w * W]
+// with W = H = 608 (Constants.MODEL_IMAGE_SIZE, not the input shape).  Shared by
+// decode_kernel and the fused GEMM epilogue so both give the same bits.
+__device__ __forceinline__ float decode_transform(int f, float v) {
+  float s = 1.f / (1.f + expf(-v));
+  if (f >= 2) s = fminf(fmaxf(s, 0.f), 1.f);
+  return s * (f == 0 ? 1.f : (f == 1 ? 79.f : 608.f));
+}
+
 // bf16 rounding of an f32 value, back in f32 (the fused quantizers quantize what the
 // unfused path would have stored as bf16)
 __device__ __forceinline__ float bf16_round(float v) {

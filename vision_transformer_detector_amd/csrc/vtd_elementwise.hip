@@ -440,11 +440,7 @@ __global__ void decode_kernel(const float* __restrict__ logits, int64_t n,
                               float* __restrict__ dets) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n * 6) return;
-  const int f = (int)(i % 6);
-  float s = 1.f / (1.f + expf(-logits[i]));
-  if (f >= 2) s = fminf(fmaxf(s, 0.f), 1.f);
-  const float scale = f == 0 ? 1.f : (f == 1 ? 79.f : 608.f);
-  dets[i] = s * scale;
+  dets[i] = decode_transform((int)(i % 6), logits[i]);
 }
 
 // transform_predictions + the thresholded detection test (vtd.py:1359-1384): one
@@ -458,9 +454,7 @@ __global__ void decode_detections_kernel(const float* __restrict__ logits, int64
   float d[6];
 #pragma unroll
   for (int f = 0; f < 6; ++f) {
-    float s = 1.f / (1.f + expf(-logits[i * 6 + f]));
-    if (f >= 2) s = fminf(fmaxf(s, 0.f), 1.f);
-    d[f] = s * (f == 0 ? 1.f : (f == 1 ? 79.f : 608.f));
+    d[f] = decode_transform(f, logits[i * 6 + f]);
     if (dets) dets[i * 6 + f] = d[f];
   }
   const float c = rintf(d[1]);

@@ -43,6 +43,7 @@ struct EpiArgs {
   float2* statout; int stat_ld;
   // out_dtype VTD_FP8 (MX-fp8 GEMMs, fast epilogue): e4m3 out + E8M0 scales [n/128][s_rows][4]
   uint8_t* sout; int64_t s_rows;
+  float* dets;                     // fused transform_predictions (N == 6, fp32 out)
 };
 
 // v of another lane of the same 16-lane row by a DPP control (0 where the source is out
@@ -141,6 +142,7 @@ __device__ __forceinline__ void epi_store(const EpiArgs& e, int M, int N, int m,
   if (e.out_dtype == VTD_F32) static_cast<float*>(e.out)[idx] = v;
   else static_cast<bf16_t*>(e.out)[idx] = f32_to_bf16(v);
   if (e.out2) static_cast<bf16_t*>(e.out2)[(int64_t)m * e.ldo2 + n] = f32_to_bf16(v);
+  if (e.dets) e.dets[(int64_t)m * 6 + n] = decode_transform(n, v);
 }
 
 __device__ __forceinline__ void gload4(i32x4 (&ra)[4], i32x4 (&rb)[4], const char* ga,
@@ -168,7 +170,7 @@ __device__ __forceinline__ void swrite4(const i32x4 (&ra)[4], const i32x4 (&rb)[
 __device__ __forceinline__ void epi_store4(const EpiArgs& e, int M, int N, int m, int n,
                                            f32x4 v) {
   if (m >= M) return;
-  const bool full = (n + 3 < N) && e.scatter_tokens <= 0 && (e.ldo & 3) == 0 &&
+  const bool full = (n + 3 < N) && e.scatter_tokens <= 0 && !e.dets && (e.ldo & 3) == 0 &&
                     (!e.resid || (e.ldr & 3) == 0) && (!e.out2 || (e.ldo2 & 3) == 0);
   if (!full) {
 #pragma unroll
@@ -1963,6 +1965,9 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
   VTD_CHECK_ARG(!epi->lnstat || (epi->colsum && reinterpret_cast<uintptr_t>(epi->lnstat) % 8 == 0 &&
                                  reinterpret_cast<uintptr_t>(epi->colsum) % 16 == 0),
                 "gemm: lnstat needs colsum (16-B aligned) and 8-B alignment");
+  VTD_CHECK_ARG(!epi->detections || (N == 6 && epi->out_dtype == VTD_F32 &&
+                                      epi->scatter_tokens <= 0),
+                "gemm: detections (fused transform_predictions) need N == 6 and an fp32 output");
   if (epi->statout && !gemm_emits_stats(M, N, dtype, epi))
     return fail(VTD_ERR_UNSUPPORTED, "gemm: statout needs full 256 x 256 tiles on the bf16 "
                                      "fast epilogues (see gemm_emits_stats)");
@@ -1971,7 +1976,7 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
             epi->out, epi->ldo, epi->out_dtype, epi->out2, epi->ldo2,
             epi->scatter_tokens, reinterpret_cast<const float2*>(epi->lnstat), epi->colsum,
             reinterpret_cast<float2*>(epi->statout), epi->stat_ld, epi->scale_out,
-            epi->scale_rows};
+            epi->scale_rows, epi->detections};
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM);
   const size_t lds = 4 * TILE_BYTES;
   ProfScope ps(stream, PROF_GEMM, flops > 0 ? flops : 2.0 * M * N * (double)K);
@@ -2023,7 +2028,7 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
       // pp2p (7) and pp3 (11), whose epilogues do not implement them
       const bool rare_ok = variant != 7 && variant != 11 &&
                            (!e.out2 || (e.ldo2 % 8 == 0 && reinterpret_cast<uintptr_t>(e.out2) % 16 == 0));
-      const bool fast = e.bias && (rare_ok || (!e.rowadd && !e.out2 && !e.lnstat)) &&
+      const bool fast = e.bias && !e.dets && (rare_ok || (!e.rowadd && !e.out2 && !e.lnstat)) &&
                         (e.scatter_tokens <= 0 || variant == 5) &&
                         e.ldo % 8 == 0 && (!e.resid || e.ldr % 8 == 0) &&
                         reinterpret_cast<uintptr_t>(e.out) % 16 == 0 &&
@@ -2161,6 +2166,8 @@ int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_
                                  reinterpret_cast<uintptr_t>(epi->colsum) % 16 == 0),
                 "gemm_mx8: lnstat needs colsum (16-B aligned) and 8-B alignment");
   if (epi->statout) return fail(VTD_ERR_UNSUPPORTED, "gemm_mx8: statout is not supported");
+  if (epi->detections)
+    return fail(VTD_ERR_UNSUPPORTED, "gemm_mx8: fused detections are not supported");
   if (epi->out_dtype == VTD_FP8 && !gemm_mx8_emits_fp8(M, N, epi))
     return fail(VTD_ERR_UNSUPPORTED, "gemm_mx8: an MX-fp8 output needs full 256 x 256 tiles, a "
                                      "bias, no residual / rowadd / out2 / scatter, ldo % 16 and "
@@ -2170,7 +2177,7 @@ int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_
             epi->out, epi->ldo, epi->out_dtype, epi->out2, epi->ldo2,
             epi->scatter_tokens, reinterpret_cast<const float2*>(epi->lnstat), epi->colsum,
             reinterpret_cast<float2*>(epi->statout), epi->stat_ld, epi->scale_out,
-            epi->scale_rows};
+            epi->scale_rows, epi->detections};
   ProfScope ps(stream, PROF_GEMM, flops > 0 ? flops : 2.0 * M * N * (double)K);
   const int tiles_m = (M + BBM - 1) / BBM, tiles_n = (N + BBN - 1) / BBN;
   static bool attr = false;

@@ -24,7 +24,6 @@ int ln_stats_finalize_launch(const float* part, int64_t rows, int slots, int D, 
 bool gemm_emits_stats(int M, int N, int dtype, const vtd_epilogue* e);
 int patches_launch(const float* img, int B, int H, int W, int C, int p, void* out, int ldo,
                    int dtype, hipStream_t st);
-int decode_launch(const float* logits, int64_t n, float* dets, hipStream_t st);
 int attention_mx8_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqkv,
                          float scale, uint8_t* q, int ldq, uint8_t* s, int64_t s_rows,
                          hipStream_t stream, double flops);
@@ -619,11 +618,8 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     vtd_epilogue e{};
     e.bias = w->b_final; e.act = VTD_ACT_NONE;
     e.out = logits; e.ldo = 6; e.out_dtype = VTD_F32;
+    e.detections = dets;                              // transform_predictions, fused
     rc = gemm_launch(HR, 6, k, a, k, w->w_final, k, dt, &e, st, 2.0 * HR * (double)kv * 6);
-    if (rc) return rc;
-  }
-  if (dets) {
-    rc = decode_launch(logits, d.head_rows, dets, st);
     if (rc) return rc;
   }
   return VTD_OK;
