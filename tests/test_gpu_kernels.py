@@ -303,6 +303,69 @@ def test_gemm_bf16_256_tile_path(L, cuda, M, N, K, act, out_dtype):
     assert err.max() < tol, (err.max(), len(bad), bad[:5].tolist())
 
 
+@pytest.mark.parametrize("M,N,K,act,resid", [
+    (50176, 768, 768, 0, True),      # attn_out at C2 B=256: 588 tiles = 2.3 rounds
+    (50176, 768, 1536, 1, True),     # mlp3
+    (12544, 1536, 3072, 1, False),   # mlp2 at B=64: 294 tiles
+    (4352, 4352, 8704, 1, False),    # head2: 289 tiles, 136 K-steps
+    (4352, 2176, 4352, 2, False),    # head3: 153 tiles (< one round), mish
+    (3000, 1544, 3072, 1, False),    # ragged M and N: generic epilogue on split tiles
+    (4100, 776, 768, 0, True),       # ragged, residual, no activation
+    (2100, 512, 256, 0, False)])     # 4 K-steps only
+def test_gemm_stream_k(L, cuda, monkeypatch, M, N, K, act, resid):
+    """Stream-K pp2 (VTD_GEMM_SK; 2 = forced): the tiles a partial last round would leave
+    idle are split over the CUs by K-steps, the partial accumulators summed by the last
+    contributor in K order.  Against fp64, against the data-parallel kernel, and
+    deterministic (the same bits on every run, whoever arrives last)."""
+    g = torch.Generator(device=cuda).manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
+    Bt = (torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g, device=cuda)
+    x0 = (4 * torch.randn(M, N, generator=g, device=cuda)).to(torch.bfloat16)
+    outs = {}
+    for mode in ("0", "2", "2b"):
+        monkeypatch.setenv("VTD_GEMM_SK", mode[0])
+        x = x0.clone()
+        _gemm(L, A, Bt, L.BF16, bias=bias, act=act, resid=x if resid else None, out=x,
+              out_dtype=1)
+        outs[mode] = x
+    ref64 = _np_act(act, (A.double() @ Bt.double().T + bias.double()).cpu().numpy())
+    if resid:
+        ref64 = ref64 + x0.double().cpu().numpy()
+    got = outs["2"].double().cpu().numpy()
+    err = np.abs(got - ref64) / np.maximum(np.abs(ref64), 1.0)
+    assert err.max() < 8e-3, err.max()
+    assert torch.equal(outs["2"], outs["2b"])                       # deterministic
+    d = (outs["2"].float() - outs["0"].float()).abs() / outs["0"].float().abs().clamp(min=1.0)
+    assert d.max().item() < 1.6e-2        # <= 2 bf16 ulps: K-split fp32 association only
+
+
+def test_gemm_stream_k_statout(L, cuda, monkeypatch):
+    """The producer-side LayerNorm partial statistics ride on the stream-K epilogue too."""
+    M, N, K = 50176, 768, 768
+    g = torch.Generator(device=cuda).manual_seed(5)
+    A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
+    Bt = (torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g, device=cuda)
+    res = {}
+    for mode in ("0", "2"):
+        monkeypatch.setenv("VTD_GEMM_SK", mode)
+        out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+        stat = torch.full((M, N // 64, 2), float("nan"), device=cuda)
+        e = L.VtdEpilogue()
+        e.bias, e.out, e.ldo, e.out_dtype = bias.data_ptr(), out.data_ptr(), N, 1
+        e.statout, e.stat_ld = stat.data_ptr(), N // 64
+        L.check(L.lib.vtd_gemm(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, L.BF16,
+                               ctypes.byref(e), L.stream_ptr()), "vtd_gemm")
+        torch.cuda.synchronize()
+        res[mode] = (out, stat)
+    out, stat = res["2"]
+    blocks = out.float().view(M, N // 64, 64)
+    assert torch.allclose(stat[..., 0], blocks.mean(-1), rtol=1e-5, atol=1e-5)
+    m2 = ((blocks - blocks.mean(-1, keepdim=True)) ** 2).sum(-1)
+    assert torch.allclose(stat[..., 1], m2, rtol=1e-4, atol=1e-4)
+
+
 def test_decode_detections_matches_oracle(L, cuda):
     """Fused decode + the MeanAveragePrecision prediction test (vtd.py:1359-1384)."""
     from vision_transformer_detector_amd import decode_detections

@@ -14,6 +14,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <mutex>
 
 #include "vtd_common.h"
 
@@ -866,13 +867,15 @@ struct PP2BufSrc {
 template <bool TR>
 __device__ __forceinline__ void pp2b_sources(PP2BufSrc& s, const bf16_t* A, int lda, int M,
                                              const bf16_t* Bt, int ldb, int N, int m0, int n0,
-                                             int wave, int lane) {
+                                             int wave, int lane, int k0 = 0) {
   // records = bytes from the tile base to the end of the operand (clamped to 32 bits); all
-  // offsets are in range because rows are clamped to the last valid row.
-  const int64_t ra_bytes = (int64_t)(M - m0) * lda * 2, rb_bytes = (int64_t)(N - n0) * ldb * 2;
-  s.ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(A + (int64_t)m0 * lda), 0,
+  // offsets are in range because rows are clamped to the last valid row.  k0: first K
+  // element of the loop (stream-K segments), folded into the base.
+  const int64_t ra_bytes = (int64_t)(M - m0) * lda * 2 - 2 * k0,
+                rb_bytes = (int64_t)(N - n0) * ldb * 2 - 2 * k0;
+  s.ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(A + (int64_t)m0 * lda + k0), 0,
                                            (int)std::min<int64_t>(ra_bytes, 0x7fffffff), 0x00020000);
-  s.rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(Bt + (int64_t)n0 * ldb), 0,
+  s.rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(Bt + (int64_t)n0 * ldb + k0), 0,
                                            (int)std::min<int64_t>(rb_bytes, 0x7fffffff), 0x00020000);
   const int prow = lane >> 3, pchunk = (lane & 7) ^ prow;
 #pragma unroll
@@ -1155,6 +1158,160 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
     }
   }
   epilogue_generic(acc, ep, lane, M, N, m_base, n_base, e);
+}
+
+// ---------------------------------------------------------------------------------
+// Stream-K pp2 ("pp2sk"): the pp2 tile, main loop and epilogues in a persistent grid of G
+// workgroups (G = CUs, a multiple of 8) that balances the last tiles over every CU instead
+// of leaving a partial final round (an N = 768 layer at C2 B = 256 is 588 tiles = 2.3
+// rounds of 256 CUs: a third of its time runs on 76 CUs).
+//   data-parallel part: tiles [0, dp_tiles), dp_tiles a multiple of G; workgroup b on XCD
+//     x = b % 8 (hardware round-robin, tools/probes/xcc_probe.hip) takes tile
+//     i G + x G/8 + b/8 in round i, so an XCD walks contiguous tiles (shared A panels);
+//   stream-K part: tiles [dp_tiles, T) are dealt to the XCDs as contiguous whole-tile
+//     blocks, and each XCD's block of K-steps is cut evenly over its G/8 workgroups.  A
+//     workgroup's range covers one or more (partial) tiles; a tile split between workgroups
+//     gets each contributor's fp32 accumulators in a private slot (slot 0 for a range's first
+//     tile, 1 for its last), and the contributor that arrives last (per-tile counter, vector
+//     atomic, no waiting anywhere: no co-residency assumption) sums the slots in K order --
+//     the same order whoever arrives last, so results are deterministic -- and runs the
+//     epilogue.  All contributors of a tile share the XCD's L2 and every slot is written at
+//     most once per launch, so workgroup-scope release / acquire fences order the slots
+//     and the counter.
+struct SkArgs {
+  int dp_tiles;
+  float* partial;     // [G][2][512 threads][32] float4
+  int* counters;      // [T], zero between launches (the last arriver resets its tile's)
+};
+
+template <int EPI, bool TR>
+__device__ __forceinline__ void pp2_tile_epilogue(const f32x4 (&acc)[8][4], char* smem, int lane,
+                                                  int wave, int M, int N, int m0, int n0,
+                                                  int m_base, int n_base, const EpiArgs& e,
+                                                  const float2* lst) {
+  if constexpr (TR) {
+    if constexpr (EPI != EPI_GENERIC) {
+      if (m0 + BBM <= M && n0 + BBN <= N) {
+        epilogue_direct<EPI>(acc, lane, m_base, n_base, e, lst);
+        return;
+      }
+    }
+    epilogue_direct_generic(acc, reinterpret_cast<float*>(smem) + wave * 32 * 68, lane, M, N,
+                            m_base, n_base, e);
+  } else {
+    float* ep = reinterpret_cast<float*>(smem) + wave * 32 * 68;
+    if constexpr (EPI != EPI_GENERIC) {
+      if (m0 + BBM <= M && n0 + BBN <= N) {
+        epilogue_fast<EPI>(acc, ep, lane, m_base, n_base, e, lst);
+        return;
+      }
+    }
+    epilogue_generic(acc, ep, lane, M, N, m_base, n_base, e);
+  }
+}
+
+template <int EPI, bool TR>
+__global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2sk_kernel(
+    int M, int N, int K, const bf16_t* __restrict__ A, int lda,
+    const bf16_t* __restrict__ Bt, int ldb, int tiles_m, int tiles_n, EpiArgs e, SkArgs sk) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int s_last;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int G = gridDim.x, GX = G >> 3;
+  const int b = blockIdx.x, x = b & 7, j = b >> 3;
+  const int T = tiles_m * tiles_n, nk = K / 64;
+  // work items: the data-parallel tiles, then this workgroup's stream-K range
+  const int ndp = sk.dp_tiles > x * GX + j ? (sk.dp_tiles - (x * GX + j) + G - 1) / G : 0;
+  const int tsk = T - sk.dp_tiles;
+  const int t_lo = sk.dp_tiles + (int)((int64_t)x * tsk / 8);
+  const int t_hi = sk.dp_tiles + (int)((int64_t)(x + 1) * tsk / 8);
+  const int S = (t_hi - t_lo) * nk;
+  const int W = max(1, (S + GX - 1) / GX);
+  const int s0 = min(j * W, S), s1 = min(s0 + W, S);
+  int item = 0, st = s0;
+#pragma unroll 1
+  while (item < ndp || st < s1) {
+    int t, k0, k1, tl = 0;
+    if (item < ndp) {
+      t = x * GX + j + item * G;
+      k0 = 0;
+      k1 = nk;
+      ++item;
+    } else {
+      tl = st / nk;
+      t = t_lo + tl;
+      k0 = st - tl * nk;
+      k1 = min(nk, s1 - tl * nk);
+      st = tl * nk + k1;
+    }
+    const int tm = t / tiles_n, tn = t - tm * tiles_n;
+    const int m0 = tm * BBM, n0 = tn * BBN;
+    PP2BufSrc src;
+    pp2b_sources<TR>(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane, k0 * 64);
+    float2 lst[2] = {float2{0.f, 0.f}, float2{0.f, 0.f}};
+    if (e.lnstat) {
+      lst[0] = e.lnstat[min(m0 + wm * 128 + lane, M - 1)];
+      lst[1] = e.lnstat[min(m0 + wm * 128 + 64 + lane, M - 1)];
+    }
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    pp2_mainloop<TR, PP2BufSrc, 0>(acc, smem, src, k1 - k0, wave, wm, wn, fr, fg);
+    if (k0 != 0 || k1 != nk) {
+      // a split tile: contributors are this XCD's workgroup slots jf..jl (K order)
+      const int jf = (tl * nk) / W, jl = (tl * nk + nk - 1) / W;
+      const int slot = (s0 / nk == tl) ? 0 : 1;
+      float4* mine = reinterpret_cast<float4*>(sk.partial) + ((int64_t)(b * 2 + slot) * BNT) * 32;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          mine[(i * 4 + q) * BNT + tid] =
+              float4{acc[i][q][0], acc[i][q][1], acc[i][q][2], acc[i][q][3]};
+      // stores acknowledged by the XCD's L2 (L1 is write-through) before the count: every
+      // contributor of a tile runs on this XCD and shares that L2, so workgroup-scope
+      // ordering suffices (an agent-scope release would write back the whole L2)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __syncthreads();
+      if (tid == 0) {
+        const int old = __hip_atomic_fetch_add(sk.counters + t, 1, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == jl - jf;
+      }
+      __syncthreads();
+      if (!s_last) continue;
+      // each slot is written at most once per launch (a range's first / last split tile),
+      // so no L1 line of it can be stale here: a workgroup-scope acquire orders the loads
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      if (tid == 0) sk.counters[t] = 0;     // ready for the next launch
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+      for (int jj = jf; jj <= jl; ++jj) {     // the same order whoever arrives last
+        const int cslot = ((jj * W) / nk == tl) ? 0 : 1;
+        const float4* p = reinterpret_cast<const float4*>(sk.partial) +
+                          ((int64_t)((jj * 8 + x) * 2 + cslot) * BNT) * 32;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 v = p[(i * 4 + q) * BNT + tid];
+            acc[i][q] += f32x4{v.x, v.y, v.z, v.w};
+          }
+      }
+    }
+    pp2_tile_epilogue<EPI, TR>(acc, smem, lane, wave, M, N, m0, n0, m0 + wm * 128,
+                               n0 + wn * 64, e, lst);
+    __syncthreads();                // the epilogue's LDS staging before the next prologue
+  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -1926,6 +2083,73 @@ int pp2_min_tiles() {
   return t;
 }
 
+// Stream-K (gemm_tn_bf16_pp2sk_kernel) for the default variant when the data-parallel grid's
+// last round would leave CUs idle: VTD_GEMM_SK = 0 off (default), 1 when the last round
+// is under 85% full, 2 always (tests).  Measured slower on every forward shape (DESIGN.md,
+// "What did not pay in round 2"): a split tile's fp32 partials (256 KiB) cost more than
+// the K-steps they balance, and ranges starting at different K-steps lose the lockstep
+// L2 sharing of the data-parallel rounds.  Returns the data-parallel tile count (a multiple
+// of G), or -1 for the plain pp2 launch.  The partial-sum slots and tile counters are
+// allocated once per device on first use (never under stream capture: a capture that
+// finds them missing runs pp2).
+struct SkWorkspace {
+  float* partial = nullptr;
+  int* counters = nullptr;
+  int tiles_cap = 0;
+};
+constexpr int kSkTilesCap = 1 << 20;
+
+int gemm_sk_mode() {       // read per call: tests switch it inside one process
+  const char* v = getenv("VTD_GEMM_SK");
+  return v ? atoi(v) : 0;
+}
+
+int sk_dp_tiles(int T, int nk, int G, hipStream_t stream, SkArgs& sk) {
+  const int mode = gemm_sk_mode();
+  if (mode == 0 || G % 8 != 0 || T > kSkTilesCap || nk < 2) return -1;
+  const int rounds = (T + G - 1) / G;
+  if (mode == 1 && (T >= (int)(0.85 * rounds * G) || nk < 4)) return -1;
+  static SkWorkspace ws[64];
+  static std::mutex mu;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    SkWorkspace& w = ws[dev];
+    if (!w.partial) {
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+        return -1;
+      float* p = nullptr;
+      int* c = nullptr;
+      if (hipMalloc(reinterpret_cast<void**>(&p), (size_t)G * 2 * BNT * 32 * 16) != hipSuccess)
+        return -1;
+      if (hipMalloc(reinterpret_cast<void**>(&c), (size_t)kSkTilesCap * sizeof(int)) != hipSuccess ||
+          hipMemset(c, 0, (size_t)kSkTilesCap * sizeof(int)) != hipSuccess) {
+        (void)hipFree(p);
+        return -1;
+      }
+      w.partial = p;
+      w.counters = c;
+      w.tiles_cap = G;
+    }
+    if (w.tiles_cap < G) return -1;
+    sk.partial = w.partial;
+    sk.counters = w.counters;
+  }
+  sk.dp_tiles = T / G >= 1 ? (T / G - 1) * G : 0;
+  return sk.dp_tiles;
+}
+
+template <int C>
+void launch_pp2sk(int G, hipStream_t stream, int M, int N, int K, const bf16_t* A, int lda,
+                  const bf16_t* Bt, int ldb, int tiles_m, int tiles_n, const EpiArgs& e,
+                  const SkArgs& sk) {
+  if constexpr (C == 4 || C == 12 || C == 5 || C == 6 || C == 13 || C == 14)
+    hipLaunchKernelGGL((gemm_tn_bf16_pp2sk_kernel<C, (C & 3) != 0>), dim3(G), dim3(BNT),
+                       2 * BSTAGE, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e, sk);
+}
+
 // Whether vtd_gemm can emit the partial LayerNorm statistics (epilogue.statout) for this
 // problem: every tile full and on the pp2b / pp2t fast epilogues with a bf16 output.
 bool gemm_emits_stats(int M, int N, int dtype, const vtd_epilogue* e) {
@@ -2008,6 +2232,15 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
       for (const void* f : fns)
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   2 * BSTAGE + EPR_BYTES);
+      const void* skfns[] = {
+          reinterpret_cast<const void*>(&gemm_tn_bf16_pp2sk_kernel<4, false>),
+          reinterpret_cast<const void*>(&gemm_tn_bf16_pp2sk_kernel<12, false>),
+          reinterpret_cast<const void*>(&gemm_tn_bf16_pp2sk_kernel<5, true>),
+          reinterpret_cast<const void*>(&gemm_tn_bf16_pp2sk_kernel<6, true>),
+          reinterpret_cast<const void*>(&gemm_tn_bf16_pp2sk_kernel<13, true>),
+          reinterpret_cast<const void*>(&gemm_tn_bf16_pp2sk_kernel<14, true>)};
+      for (const void* f : skfns)        // + 4 B of static LDS (the last-arriver flag)
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
       attr = true;
     }
     const int variant = gemm_variant();
@@ -2082,10 +2315,20 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
         VTD_LAUNCH_CHECK("gemm");
         return VTD_OK;
       }
+      // stream-K on the bf16-output epilogues of the default variant (act: transposed
+      // accumulators, as pp2t; none: pp2b)
+      SkArgs sk{};
+      const bool sk_code = code == 4 || code == 12 || code == 5 || code == 6 || code == 13 ||
+                           code == 14;
+      const int skdp = variant == 10 && sk_code
+                           ? sk_dp_tiles(tiles_m * tiles_n, K / 64, num_cu, stream, sk)
+                           : -1;
       switch (code) {
 #define VTD_PP_CASE(C)                                                                      \
   case C:                                                                                   \
-    if (pp2p)                                                                               \
+    if (skdp >= 0)                                                                          \
+      launch_pp2sk<C>(num_cu, stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e, sk); \
+    else if (pp2p)                                                                          \
       hipLaunchKernelGGL((gemm_tn_bf16_pp2p_kernel<C>), gp, b, 2 * BSTAGE + EPR_BYTES,      \
                          stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);         \
     else if (pp2b)                                                                          \
