@@ -186,7 +186,11 @@ def _attn_ref(qkv, B, N, H, dk, dkp):
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("B,N,H,dk", [(2, 196, 3, 64), (1, 70, 2, 40), (1, 1, 1, 32),
-                                      (1, 333, 2, 128), (1, 1296, 1, 40), (1, 64, 4, 20)])
+                                      (1, 333, 2, 128), (1, 1296, 1, 40), (1, 64, 4, 20),
+                                      # persistent kernel (dkp 64, 128 < N <= 256): several
+                                      # pairs per workgroup, N not a multiple of 32 / 8
+                                      (40, 196, 12, 64), (3, 129, 5, 64), (2, 256, 2, 64),
+                                      (1, 200, 3, 50), (700, 131, 1, 64)])
 def test_attention(L, cuda, dtype, B, N, H, dk):
     code, tdt = _dt(L, dtype)
     dkp = 32 if dk <= 32 else (64 if dk <= 64 else 128)
@@ -211,6 +215,32 @@ def test_attention(L, cuda, dtype, B, N, H, dk):
     tol = 2e-5 if dtype == "f32" else 2e-2
     assert np.abs(got[..., :dk] - exp).max() < tol * max(1.0, np.abs(exp).max())
     assert (got[..., dk:] == 0).all()
+
+
+@pytest.mark.parametrize("B,N,H", [(256, 196, 12), (5, 129, 7), (3, 256, 4), (1, 250, 1)])
+def test_attention_persistent_equals_per_pair_kernel(L, cuda, monkeypatch, B, N, H):
+    """The persistent short-sequence kernel (VTD_ATTN_VARIANT 4, the default for dkp 64 and
+    128 < N <= 256) against the per-(image, head) kernel, at the C2 shape (3072 pairs, 12 per
+    workgroup) and ragged ones.  Its softmax takes the row's true max in one pass (all keys
+    are in LDS) where the streaming kernel keeps a deferred running max, so P rounds to bf16
+    differently: equal to within bf16 rounding of P (both are checked against fp64 in
+    test_attention)."""
+    dkp = 64
+    ld = 3 * H * dkp + 8
+    g = torch.Generator().manual_seed(N + H)
+    qkv = (torch.randn(B * N, ld, generator=g) * 1.5).to(torch.bfloat16).to(cuda)
+    outs = []
+    for variant in ("2", "4"):
+        monkeypatch.setenv("VTD_ATTN_VARIANT", variant)
+        o = torch.full((B * N, H * dkp + 16), float("nan"), dtype=torch.bfloat16, device=cuda)
+        L.check(L.lib.vtd_attention(qkv.data_ptr(), B, N, H, dkp, ld, 0.125, o.data_ptr(),
+                                    H * dkp + 16, L.BF16, L.stream_ptr()), "attention")
+        torch.cuda.synchronize()
+        outs.append(o.cpu())
+    a, b = outs[0][:, :H * dkp].float(), outs[1][:, :H * dkp].float()
+    assert torch.isfinite(b).all()
+    assert (a - b).abs().max().item() <= 1e-2 * max(1.0, a.abs().max().item())
+    assert torch.isnan(outs[1][:, H * dkp:].float()).all()     # nothing written past ldo's heads
 
 
 def test_attention_uniform_kat(L, cuda):

@@ -232,6 +232,16 @@ __global__ __launch_bounds__(512) void attention_kernel(
 // (lane 4q+p of a 16-lane group addresses key q, d 4p..4p+3 of the block).
 // V row stride DKP*2 + 64 B shifts consecutive keys by 16 mod 64 banks, so the 4 rows
 // x 64 B of a 32-lane tr-read half cover all 64 banks once (conflict-free for DKP 64/128).
+// lanes l and l ^ 32 combined by one v_permlane32_swap (no LDS round trip): after the swap
+// the two results hold x[l] and x[l ^ 32] in some order, so max / sum of them is the pair's
+__device__ __forceinline__ float pair_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float pair_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 template <int DKP>
 struct AttnBf16Cfg {
   static constexpr int KC = 64;                       // keys per chunk
@@ -482,6 +492,267 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Persistent short-sequence kernel (bf16, DKP = 64, 128 < N <= 256: the C2 shape N = 196).
+// At N = 196 the per-(image, head) kernel above spends most of a workgroup's life waiting:
+// an exposed Q + first-chunk load, then one barrier + one register-staged chunk per 64 keys.
+// Here one workgroup per CU walks the (image, head) pairs p = blockIdx.x + i * gridDim.x and
+// the loads never stop:
+//   - a pair's whole K and V (NR = N rounded up to 32 rows of 128 B each) arrive by LDS-DMA
+//     (buffer_load ... lds, 8 rows = 1 KiB per wave-instruction, no VGPR staging) into one of
+//     two slots, issued while the previous pair is computed; its Q arrives the same way in a
+//     third area, one pair ahead, and goes to registers at the top of the pair;
+//   - the compute of a pair reads only LDS: no barrier between its key chunks;
+//   - O is restaged through the pair's own slot (after the compute's barrier) and stored as
+//     whole 128-B rows by buffer stores whose range check drops the rows >= N, so every wave
+//     issues exactly 4 stores per pair: the next pair's wait is `vmcnt(4)` (the DMAs landed,
+//     the stores may still fly).
+// LDS images are lane-linear (the DMA writes base + 16 * lane) and swizzled on the source
+// address: K and Q rows chunk ^ ((row >> 1) & 7) (the 16 rows of a ds_read_b128 lane group hit
+// 16 distinct 16-B bank slots), V rows chunk ^ (((row >> 1) & 1) << 2) (the 4 rows x 64 B of
+// a ds_read_b64_tr_b16 half-wave cover the 64 banks once).  Same arithmetic and operation
+// order as attention_bf16_kernel: per-image results are identical (tested).
+// Waits: counted vmcnt + raw s_barrier only (a __syncthreads fence would drain the DMAs).
+__device__ __forceinline__ int swz_kq(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ int swz_v(int row) { return ((row >> 1) & 1) << 2; }
+
+template <int NB>   // key blocks of 32: N in (32 (NB - 1), 32 NB]
+__global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
+    const bf16_t* __restrict__ qkv, int npairs, int N, int heads, int ldqkv, float scale_log2,
+    bf16_t* __restrict__ out, int ldo, int diag) {
+  // diag (timing diagnostics only, wrong outputs): bit 0 = no DMA after the first pair (compute
+  // on stale slots), bit 1 = no compute (DMA, restage and stores only)
+  constexpr int DKP = 64;
+  typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+  typedef __attribute__((address_space(3))) void lds_void_t;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6, half = lane >> 5, col = lane & 31;
+  const int NR = (N + 31) & ~31;
+  const int SLOT = 2 * NR * 128;                 // K image, then V image
+  char* const qarea = smem + 2 * SLOT;
+  const int inner = heads * DKP;
+  const int q0 = wave * 32;
+  const bool active = q0 < N && !(diag & 2);
+  const int G = gridDim.x;
+  const int ngroups = NR >> 3;                   // 8-row groups per matrix
+  const int lrow = lane >> 3, lchunk = lane & 7;
+  const uint32_t lds_base =
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(smem);
+
+  // DMA of one matrix (part 0 = Q, 1 = K, 2 = V) of pair p into dst
+  auto issue = [&](int p, int part, char* dst) {
+    const int b = p / heads, h = p - b * heads;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(qkv + (int64_t)b * N * ldqkv), 0, N * ldqkv * 2, 0x00020000);
+    const int colb = (part * inner + h * DKP) * 2;
+    for (int g = wave; g < ngroups; g += 8) {
+      const int r = g * 8 + lrow;
+      const int sw = part == 2 ? swz_v(r) : swz_kq(r);
+      const int voff = min(r, N - 1) * ldqkv * 2 + colb + ((lchunk ^ sw) << 4);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + g * 1024), 16, voff, 0, 0,
+                                               0);
+    }
+  };
+
+  int p = blockIdx.x;
+  if (p >= npairs) return;                       // uniform per workgroup
+  issue(p, 1, smem);
+  issue(p, 2, smem + NR * 128);
+  issue(p, 0, qarea);
+  const int tr_key = 4 * half + ((lane & 15) >> 2);
+  const int tr_byte = ((lane >> 4) & 1) * 32 + (lane & 3) * 8;   // within a 64-B d block
+  for (int it = 0; p < npairs; p += G, ++it) {
+    char* const kl = smem + (it & 1) * SLOT;
+    const uint32_t kl_addr = lds_base + (it & 1) * SLOT, vl_addr = kl_addr + NR * 128;
+    if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // previous pair's O stores may fly
+    __builtin_amdgcn_s_barrier();
+    bf16x8 qf[4];
+    if (active) {
+      const int row = q0 + col;
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+        qf[st] = *reinterpret_cast<const bf16x8*>(qarea + row * 128 +
+                                                   (((st * 2 + half) ^ swz_kq(row)) << 4));
+    }
+    const int pn = p + G;
+    const bool fetch = pn < npairs && !(diag & 1);
+    if (fetch) {
+      char* const kn = smem + ((it + 1) & 1) * SLOT;
+      issue(pn, 1, kn);
+      issue(pn, 2, kn + NR * 128);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // Q fragments in registers
+    __builtin_amdgcn_s_barrier();
+    if (fetch) issue(pn, 0, qarea);
+
+    f32x16 o[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+    float l_run = 0.f;
+    if (active) {
+      // ---- all NB key blocks of S^T = K . Q^T at once (NB independent MFMA chains): every
+      // key is in LDS, so the softmax takes the row's true max in one pass (no running max)
+      f32x16 s[NB];
+      const int swk = swz_kq(col);             // (row >> 1) & 7 with row = 32 kb + col
+#pragma unroll
+      for (int kb = 0; kb < NB; ++kb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+        const char* krow = kl + (kb * 32 + col) * 128;
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+          s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              *reinterpret_cast<const bf16x8*>(krow + (((st * 2 + half) ^ swk) << 4)), qf[st],
+              s[kb], 0, 0, 0);
+      }
+      if (N < NB * 32) {                        // keys >= N of the last block
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = (NB - 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+          if (key >= N) s[NB - 1][r] = -INFINITY;
+        }
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < NB; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
+      mx = pair_max(mx) * scale_log2;
+      // ---- P = exp2(S c - max) block by block, each block's four O^T += V^T . P^T MFMAs
+      // issued right after its exponentials: the matrix core runs them while the VALU
+      // exponentiates the next block (scalar fma / add: packed f32 ops cost more beside MFMAs)
+      // V^T fragments by inline-asm tr-reads one block ahead (the compiler's own tr-read
+      // would be treated as aliasing the in-flight LDS-DMA and wait vmcnt(0) for the next
+      // pair); lane-constant part of the swizzled address hoisted
+      const int swv = swz_v(tr_key);            // rows 32 kb + 16 st + tr_key (+ 8): same
+      uint32_t va[2];
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        const int byte = db * 64 + tr_byte;
+        va[db] = vl_addr + tr_key * 128 + (((byte >> 4) ^ swv) << 4) + (byte & 15);
+      }
+      bf16x4 vf[2][2][2][2];                    // [kb parity][st][db][lo / hi]
+      auto vread = [&](int kb, bf16x4 (&f)[2][2][2]) {
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            const uint32_t a = va[db] + (kb * 32 + 16 * st) * 128;
+            asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(f[st][db][0]) : "v"(a));
+            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:1024" : "=v"(f[st][db][1]) : "v"(a));
+          }
+      };
+      vread(0, vf[0]);
+      float ps0 = 0.f, ps1 = 0.f;
+      const float nmx = -mx;
+#pragma unroll
+      for (int kb = 0; kb < NB; ++kb) {
+        bf16x8 pb[2];
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          float e[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            e[j] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][8 * st + j], scale_log2, nmx));
+            if (j & 1) ps1 += e[j];
+            else ps0 += e[j];
+          }
+          pb[st] = __builtin_bit_cast(bf16x8, i32x4{(int)pack_bf16x2(e[0], e[1]),
+                                                    (int)pack_bf16x2(e[2], e[3]),
+                                                    (int)pack_bf16x2(e[4], e[5]),
+                                                    (int)pack_bf16x2(e[6], e[7])});
+        }
+        if (kb + 1 < NB) {
+          vread(kb + 1, vf[(kb + 1) & 1]);
+          asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            const bf16x4 lo = vf[kb & 1][st][db][0], hi = vf[kb & 1][st][db][1];
+            const bf16x8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb[st], o[db], 0, 0, 0);
+          }
+      }
+      l_run = ps0 + ps1;
+    }
+    // every wave done reading this slot's K / V: restage O in it, store whole rows
+    __builtin_amdgcn_s_barrier();
+    const float inv = 1.f / pair_sum(l_run);
+    char* const wst = kl + wave * (32 * 144);
+    if (active) {
+      // inline asm for the same reason as the tr-reads (a compiler ds_write would wait
+      // vmcnt(0) for the next pair's DMA); "memory" keeps the row reads below after them
+      const uint32_t wa = kl_addr + wave * (32 * 144) + col * 144 + 8 * half;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const uint2 v = {pack_bf16x2(o[db][4 * g + 0] * inv, o[db][4 * g + 1] * inv),
+                           pack_bf16x2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv)};
+          asm volatile("ds_write_b64 %0, %1 offset:%2" ::"v"(wa), "v"(v), "n"((db * 32 + 8 * g) * 2)
+                       : "memory");
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // wave-local: own writes landed
+    {
+      const int b = p / heads, h = p - b * heads;
+      const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+          out + (int64_t)b * N * ldo, 0, N * ldo * 2, 0x00020000);
+#pragma unroll
+      for (int pass = 0; pass < 4; ++pass) {
+        const int r = pass * 8 + lrow;
+        const i32x4 v = *reinterpret_cast<const i32x4*>(wst + r * 144 + lchunk * 16);
+        // rows >= N (and every row of an inactive wave) fall outside the range: dropped
+        __builtin_amdgcn_raw_buffer_store_b128(v, ro, ((q0 + r) * ldo + h * DKP + lchunk * 8) * 2,
+                                               0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+int launch_bf16_ps(const void* qkv, int B, int N, int heads, int ldqkv, float scale, void* out,
+                   int ldo, hipStream_t stream) {
+  const int NR = (N + 31) & ~31;
+  const int lds = 5 * NR * 128;
+  static int ncu = 0;
+  static bool attr_set = false;
+  if (!attr_set) {
+    for (const void* f : {reinterpret_cast<const void*>(&attention_bf16_ps_kernel<5>),
+                          reinterpret_cast<const void*>(&attention_bf16_ps_kernel<6>),
+                          reinterpret_cast<const void*>(&attention_bf16_ps_kernel<7>),
+                          reinterpret_cast<const void*>(&attention_bf16_ps_kernel<8>)})
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 5 * 256 * 128);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu <= 0) ncu = 256;
+    attr_set = true;
+  }
+  const int npairs = B * heads;
+  const int grid = std::min(npairs, ncu);
+  const char* denv = getenv("VTD_ATTN_DIAG");
+  const int diag = denv ? atoi(denv) : 0;
+  auto* kern = NR == 160 ? attention_bf16_ps_kernel<5>
+               : NR == 192 ? attention_bf16_ps_kernel<6>
+               : NR == 224 ? attention_bf16_ps_kernel<7>
+                           : attention_bf16_ps_kernel<8>;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, stream, static_cast<const bf16_t*>(qkv),
+                     npairs, N, heads, ldqkv, scale * 1.4426950408889634f,
+                     static_cast<bf16_t*>(out), ldo, diag);
+  VTD_LAUNCH_CHECK("attention_bf16_ps");
+  return VTD_OK;
+}
+
 template <int DKP, int NWG, bool MX8 = false>
 int launch_bf16_v2(const void* qkv, int B, int N, int heads, int ldqkv, float scale,
                    void* out, int ldo, hipStream_t stream, uint8_t* s8 = nullptr,
@@ -539,10 +810,14 @@ int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqk
   ProfScope ps(stream, PROF_ATTN,
                flops > 0 ? flops : 4.0 * B * heads * (double)N * N * dkp);
   if (dtype == VTD_BF16) {
-    static const int v1 = [] {
-      const char* v = getenv("VTD_ATTN_VARIANT");
-      return v ? atoi(v) : 2;
-    }();
+    // read per call (tests A/B the variants in one process; 12 getenv per forward)
+    const char* venv = getenv("VTD_ATTN_VARIANT");
+    const int v1 = venv ? atoi(venv) : 4;
+    // 4 (default): the persistent kernel where it applies (dkp 64, 128 < N <= 256, whole
+    // 128-B rows and 16-B aligned row pitches), else as 2
+    if (v1 == 4 && dkp == 64 && N > 128 && N <= 256 && ldqkv % 8 == 0 && ldo % 8 == 0 &&
+        (int64_t)N * ldqkv * 2 < INT32_MAX && (int64_t)N * ldo * 2 < INT32_MAX)
+      return launch_bf16_ps(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
     if (v1 == 1) {
       if (dkp == 32) return launch<bf16_t, 32>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
       if (dkp == 64) return launch<bf16_t, 64>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
