@@ -45,7 +45,31 @@ struct EpiArgs {
   // out_dtype VTD_FP8 (MX-fp8 GEMMs, fast epilogue): e4m3 out + E8M0 scales [n/128][s_rows][4]
   uint8_t* sout; int64_t s_rows;
   float* dets;                     // fused transform_predictions (N == 6, fp32 out)
+  // tile order (pp2): 0 = row-major (an XCD walks all n-tiles of consecutive m-rows); g > 0 =
+  // n-groups of g tiles, m-rows inside a group (an XCD keeps a group's weight panels in L2)
+  int ngw;
 };
+
+// tile index -> (tm, tn) for EpiArgs::ngw (bijective; the last n-group may be narrower)
+__device__ __forceinline__ void tile_coords(int tile, int tiles_m, int tiles_n, int ngw, int& tm,
+                                            int& tn) {
+  if (ngw <= 0 || ngw >= tiles_n) {
+    tm = tile / tiles_n;
+    tn = tile - tm * tiles_n;
+    return;
+  }
+  const int full = tiles_n / ngw, gsz = tiles_m * ngw;
+  const int g = tile / gsz;
+  if (g < full) {
+    const int r = tile - g * gsz;
+    tm = r / ngw;
+    tn = g * ngw + (r - tm * ngw);
+  } else {
+    const int lw = tiles_n - full * ngw, r = tile - full * gsz;
+    tm = r / lw;
+    tn = full * ngw + (r - tm * lw);
+  }
+}
 
 // v of another lane of the same 16-lane row by a DPP control (0 where the source is out
 // of the row)
@@ -1116,7 +1140,8 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int tm = tile / tiles_n, tn = tile - (tile / tiles_n) * tiles_n;
+  int tm, tn;
+  tile_coords(tile, tiles_m, tiles_n, e.ngw, tm, tn);
   const int m0 = tm * BBM, n0 = tn * BBN;
   using Src = std::conditional_t<BUF, PP2BufSrc, PP2Src>;
   Src src;
@@ -2201,6 +2226,15 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
             epi->scatter_tokens, reinterpret_cast<const float2*>(epi->lnstat), epi->colsum,
             reinterpret_cast<float2*>(epi->statout), epi->stat_ld, epi->scale_out,
             epi->scale_rows, epi->detections};
+  {
+    // pp2 tile order: weight-panel groups of 4 n-tiles (3 at 6) walked down the m-rows keep
+    // an XCD's B panels in its L2 (measured per shape, tools/r2_ngw*.sh: qkv / mlp1 / head1
+    // -3.3..-4 %, mlp2 -1.7 %); narrower N stays row-major.  VTD_GEMM_NGW overrides (read per
+    // call: A/B in one process; 0 = row-major)
+    const int tn = (N + BBN - 1) / BBN;
+    const char* v = getenv("VTD_GEMM_NGW");
+    e.ngw = v ? atoi(v) : tn >= 8 ? 4 : tn == 6 ? 3 : 0;
+  }
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM);
   const size_t lds = 4 * TILE_BYTES;
   ProfScope ps(stream, PROF_GEMM, flops > 0 ? flops : 2.0 * M * N * (double)K);
