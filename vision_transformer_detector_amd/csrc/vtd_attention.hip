@@ -523,7 +523,6 @@ __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
   // diag (timing diagnostics only, wrong outputs): bit 0 = no DMA after the first pair (compute
   // on stale slots), bit 1 = no compute (DMA, restage and stores only)
   constexpr int DKP = 64;
-  typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
   typedef __attribute__((address_space(3))) void lds_void_t;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;

@@ -50,6 +50,16 @@ struct EpiArgs {
   int ngw;
 };
 
+// bf16 output row vector store of the fast epilogues; build-time A/B knob VTD_OUT_NT: 1 =
+// non-temporal (streaming) stores, so the output stream does not evict the weight panels
+#ifndef VTD_OUT_NT
+#define VTD_OUT_NT 0
+#endif
+__device__ __forceinline__ void store_out16(void* p, i32x4 v) {
+  if constexpr (VTD_OUT_NT) __builtin_nontemporal_store(v, reinterpret_cast<i32x4*>(p));
+  else *reinterpret_cast<i32x4*>(p) = v;
+}
+
 // tile index -> (tm, tn) for EpiArgs::ngw (bijective; the last n-group may be narrower)
 __device__ __forceinline__ void tile_coords(int tile, int tiles_m, int tiles_n, int ngw, int& tm,
                                             int& tn) {
@@ -631,7 +641,7 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
         }
         const i32x4 o = {(int)pack_bf16x2(v0[0], v0[1]), (int)pack_bf16x2(v0[2], v0[3]),
                          (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
-        *reinterpret_cast<i32x4*>(static_cast<bf16_t*>(e.out) + idx) = o;
+        store_out16(static_cast<bf16_t*>(e.out) + idx, o);
         if (e.statout) {           // the row's 64 columns live in 8 consecutive lanes
           // block mean, then the centred sum of squares (DPP sums, no LDS traffic)
           const float mean = sum8_dpp(bf16x8_sum(o)) * (1.f / 64.f);
@@ -1081,7 +1091,7 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
         if constexpr (OUT_BF16) {
           const i32x4 o = {(int)pack_bf16x2(v0[0], v0[1]), (int)pack_bf16x2(v0[2], v0[3]),
                            (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
-          *reinterpret_cast<i32x4*>(static_cast<bf16_t*>(e.out) + idx) = o;
+          store_out16(static_cast<bf16_t*>(e.out) + idx, o);
           if (e.statout) {
             ob[jp] = o;
             tsum += bf16x8_sum(o);
@@ -1394,7 +1404,7 @@ __device__ __forceinline__ void epilogue_fast_x(const f32x4 (&acc)[8][4], float*
       if constexpr (OUT_BF16) {
         const i32x4 o = {(int)pack_bf16x2(v0[0], v0[1]), (int)pack_bf16x2(v0[2], v0[3]),
                          (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
-        *reinterpret_cast<i32x4*>(static_cast<bf16_t*>(e.out) + idx) = o;
+        store_out16(static_cast<bf16_t*>(e.out) + idx, o);
       } else {
         float* op = static_cast<float*>(e.out) + idx;
         *reinterpret_cast<f32x4*>(op) = v0;
@@ -1772,7 +1782,8 @@ __global__ __launch_bounds__(BNT) void gemm_mx8_kernel(
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int tm = tile / tiles_n, tn = tile - (tile / tiles_n) * tiles_n;
+  int tm, tn;
+  tile_coords(tile, tiles_m, tiles_n, e.ngw, tm, tn);
   const int m0 = tm * BBM, n0 = tn * BBN;
 
   // operand DMA through buffer resources based at the tile's first row: wave fills tile
@@ -1970,7 +1981,8 @@ __global__ __launch_bounds__(BNT) void gemm_mx8_pp_kernel(
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int tm = tile / tiles_n, tn = tile - (tile / tiles_n) * tiles_n;
+  int tm, tn;
+  tile_coords(tile, tiles_m, tiles_n, e.ngw, tm, tn);
   const int m0 = tm * BBM, n0 = tn * BBN;
   MxpSrc src;
   {
@@ -2457,6 +2469,10 @@ int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_
             epi->scale_rows, epi->detections};
   ProfScope ps(stream, PROF_GEMM, flops > 0 ? flops : 2.0 * M * N * (double)K);
   const int tiles_m = (M + BBM - 1) / BBM, tiles_n = (N + BBN - 1) / BBN;
+  {
+    const char* v = getenv("VTD_GEMM_NGW");     // tile order as in gemm_launch
+    e.ngw = v ? atoi(v) : tiles_n >= 8 ? 4 : tiles_n == 6 ? 3 : 0;
+  }
   static bool attr = false;
   if (!attr) {
 #define VTD_MX_FN(C) reinterpret_cast<const void*>(&gemm_mx8_kernel<C>), \
