@@ -190,7 +190,7 @@ def _attn_ref(qkv, B, N, H, dk, dkp):
                                       # persistent kernel (dkp 64, 128 < N <= 256): several
                                       # pairs per workgroup, N not a multiple of 32 / 8
                                       (40, 196, 12, 64), (3, 129, 5, 64), (2, 256, 2, 64),
-                                      (1, 200, 3, 50), (700, 131, 1, 64)])
+                                      (1, 200, 3, 50), (700, 131, 1, 64), (2, 224, 3, 64)])
 def test_attention(L, cuda, dtype, B, N, H, dk):
     code, tdt = _dt(L, dtype)
     dkp = 32 if dk <= 32 else (64 if dk <= 64 else 128)
@@ -217,7 +217,7 @@ def test_attention(L, cuda, dtype, B, N, H, dk):
     assert (got[..., dk:] == 0).all()
 
 
-@pytest.mark.parametrize("B,N,H", [(256, 196, 12), (5, 129, 7), (3, 256, 4), (1, 250, 1)])
+@pytest.mark.parametrize("B,N,H", [(256, 196, 12), (5, 129, 7), (3, 224, 4), (1, 161, 1)])
 def test_attention_persistent_equals_per_pair_kernel(L, cuda, monkeypatch, B, N, H):
     """The persistent short-sequence kernel (VTD_ATTN_VARIANT 4, the default for dkp 64 and
     128 < N <= 256) against the per-(image, head) kernel, at the C2 shape (3072 pairs, 12 per
