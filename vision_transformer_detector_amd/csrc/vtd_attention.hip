@@ -738,7 +738,10 @@ int launch_bf16_ps(const void* qkv, int B, int N, int heads, int ldqkv, float sc
     attr_set = true;
   }
   const int npairs = B * heads;
-  const int grid = std::min(npairs, ncu);
+  // workgroups: one per CU (VTD_ATTN_GRID overrides, read per call: A/B of co-running
+  // the two micro-batch streams' attention on disjoint halves of the chip)
+  const char* genv = getenv("VTD_ATTN_GRID");
+  const int grid = std::min(npairs, genv && atoi(genv) > 0 ? atoi(genv) : ncu);
   const char* denv = getenv("VTD_ATTN_DIAG");
   const int diag = denv ? atoi(denv) : 0;
   auto* kern = NR == 160 ? attention_bf16_ps_kernel<5>
