@@ -45,6 +45,10 @@ struct EpiArgs {
   // out_dtype VTD_FP8 (MX-fp8 GEMMs, fast epilogue): e4m3 out + E8M0 scales [n/128][s_rows][4]
   uint8_t* sout; int64_t s_rows;
   float* dets;                     // fused transform_predictions (N == 6, fp32 out)
+  // fused LayerNorm finalize (pp2 consumers of the fold path): the producer's per-row
+  // per-64-column centred partials, `lnslots` per row; the kernel merges them itself (as
+  // ln_stats_finalize_kernel) instead of reading lnstat
+  const float2* lnpart; int lnslots; int lnD; float lneps;
   // tile order (pp2): 0 = row-major (an XCD walks all n-tiles of consecutive m-rows); g > 0 =
   // n-groups of g tiles, m-rows inside a group (an XCD keeps a group's weight panels in L2)
   int ngw;
@@ -1162,7 +1166,17 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
   // LayerNorm-fold row statistics of the wave's 128 rows: issued before the K loop (the
   // oldest vector-memory op, so the loop's counted waits retire it), used in the epilogue
   float2 lst[2] = {float2{0.f, 0.f}, float2{0.f, 0.f}};
-  if (e.lnstat) {
+  if (e.lnpart) {
+    // fused finalize: the tile's 256 rows of partials (contiguous, 16 B per lane) go to LDS
+    // past the two stages by DMA, issued before the prologue's DMAs (its counted wait
+    // retires them); merged after the K loop
+    const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float2*>(e.lnpart + (int64_t)m0 * e.lnslots), 0,
+        (M - m0) * e.lnslots * 8, 0x00020000);
+    for (int c = wave; c < 2 * e.lnslots; c += 8)   // 256 rows x slots x 8 B / 1 KiB
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rp, (lds_void_t*)(smem + 2 * BSTAGE + c * 1024), 16,
+                                               c * 1024 + lane * 16, 0, 0, 0);
+  } else if (e.lnstat) {
     lst[0] = e.lnstat[min(m0 + wm * 128 + lane, M - 1)];
     lst[1] = e.lnstat[min(m0 + wm * 128 + 64 + lane, M - 1)];
   }
@@ -1174,6 +1188,31 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
   const int fr = lane & 15, fg = lane >> 4;
   pp2_mainloop<TR, Src, DG>(acc, smem, src, K / 64, wave, wm, wn, fr, fg);
   const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
+  if (e.lnpart) {
+    // the arithmetic of ln_stats_finalize_kernel, row by row (the loop's barriers made every
+    // wave's DMA visible)
+    const int S = e.lnslots;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const float2* pr =
+          reinterpret_cast<const float2*>(smem + 2 * BSTAGE) + (wm * 128 + hh * 64 + lane) * S;
+      const float mb = pr[0].x;
+      float ds = 0.f, qq = 0.f;
+      for (int b = 0; b < S; ++b) {
+        const float2 t = pr[b];
+        ds += t.x - mb;
+        qq += t.y;
+      }
+      const float dmean = ds / S;
+      float between = 0.f;
+      for (int b = 0; b < S; ++b) {
+        const float dv = (pr[b].x - mb) - dmean;
+        between += dv * dv;
+      }
+      const float var = (qq + 64.f * between) / e.lnD;
+      lst[hh] = float2{mb + dmean, 1.f / sqrtf(var + e.lneps)};
+    }
+  }
   if constexpr (TR) {
     if constexpr (EPI != EPI_GENERIC) {
       if (m0 + BBM <= M && n0 + BBN <= N) {
@@ -2210,8 +2249,24 @@ bool gemm_mx8_emits_fp8(int M, int N, const vtd_epilogue* e) {
          e->scale_out && e->scale_rows >= M && e->scale_rows % 4 == 0;
 }
 
+int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
+                   int dtype, const vtd_epilogue* epi, hipStream_t stream, double flops,
+                   const float* lnpart, int lnslots, int lnD, float lneps);
+int ln_stats_finalize_launch(const float* part, int64_t rows, int slots, int D, float eps,
+                             float* stat, hipStream_t st);
+
 int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
                 int dtype, const vtd_epilogue* epi, hipStream_t stream, double flops) {
+  return gemm_launch_ln(M, N, K, A, lda, Bt, ldb, dtype, epi, stream, flops, nullptr, 0, 0, 0.f);
+}
+
+// A GEMM whose LayerNorm-fold row statistics (epi->lnstat) are still the producer's partials
+// (lnpart, lnslots per row; the fold path): the pp2 kernels merge them themselves when every
+// tile is full and the default fast epilogue runs; otherwise ln_stats_finalize first writes
+// epi->lnstat (the unfused sequence).  lnpart == nullptr: a plain gemm_launch.
+int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
+                   int dtype, const vtd_epilogue* epi, hipStream_t stream, double flops,
+                   const float* lnpart, int lnslots, int lnD, float lneps) {
   VTD_CHECK_ARG(M > 0 && N > 0 && K > 0, "gemm: M, N, K must be positive");
   VTD_CHECK_ARG(K % VTD_KALIGN == 0, "gemm: K must be a multiple of VTD_KALIGN");
   VTD_CHECK_ARG(A && Bt && epi && epi->out, "gemm: null pointer");
@@ -2246,6 +2301,15 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
     const int tn = (N + BBN - 1) / BBN;
     const char* v = getenv("VTD_GEMM_NGW");
     e.ngw = v ? atoi(v) : tn >= 8 ? 4 : tn == 6 ? 3 : 0;
+  }
+  // fused LayerNorm finalize only on the default pp2 path (see below); elsewhere the
+  // finalize kernel writes lnstat first
+  if (lnpart && !(dtype == VTD_BF16 && N > 64 && gemm_variant() == 10 &&
+                  ((M + BBM - 1) / BBM) * ((N + BBN - 1) / BBN) >= pp2_min_tiles())) {
+    const int rc = ln_stats_finalize_launch(lnpart, M, lnslots, lnD, lneps,
+                                            const_cast<float*>(epi->lnstat), stream);
+    if (rc) return rc;
+    lnpart = nullptr;
   }
   dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM);
   const size_t lds = 4 * TILE_BYTES;
@@ -2369,6 +2433,20 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
       const int skdp = variant == 10 && sk_code
                            ? sk_dp_tiles(tiles_m * tiles_n, K / 64, num_cu, stream, sk)
                            : -1;
+      if (lnpart) {
+        if (variant == 10 && code != EPI_GENERIC && skdp < 0 && M % BBM == 0 && N % BBN == 0 &&
+            2 * lnslots * 1024 <= EPR_BYTES) {
+          e.lnpart = reinterpret_cast<const float2*>(lnpart);
+          e.lnslots = lnslots; e.lnD = lnD; e.lneps = lneps;
+        } else {
+          const int rc = ln_stats_finalize_launch(lnpart, M, lnslots, lnD, lneps,
+                                                  const_cast<float*>(reinterpret_cast<const float*>(e.lnstat)),
+                                                  stream);
+          if (rc) return rc;
+        }
+        lnpart = nullptr;
+      }
+      const int lds_pp2 = 2 * BSTAGE + (e.lnpart ? 2 * e.lnslots * 1024 : 0);
       switch (code) {
 #define VTD_PP_CASE(C)                                                                      \
   case C:                                                                                   \
@@ -2378,10 +2456,10 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
       hipLaunchKernelGGL((gemm_tn_bf16_pp2p_kernel<C>), gp, b, 2 * BSTAGE + EPR_BYTES,      \
                          stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);         \
     else if (pp2b)                                                                          \
-      hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, true>), g, b, 2 * BSTAGE, stream, M,   \
+      hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, true>), g, b, lds_pp2, stream, M,      \
                          N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);                    \
     else if (pp2t)                                                                          \
-      hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, true, true>), g, b, 2 * BSTAGE, stream,\
+      hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, true, true>), g, b, lds_pp2, stream,   \
                          M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);                 \
     else if (pp2)                                                                           \
       hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C>), g, b, 2 * BSTAGE, stream, M, N, K,  \

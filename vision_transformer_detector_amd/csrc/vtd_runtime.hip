@@ -12,6 +12,9 @@ namespace vtd {
 
 int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
                 int dtype, const vtd_epilogue* epi, hipStream_t stream, double flops);
+int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
+                   int dtype, const vtd_epilogue* epi, hipStream_t stream, double flops,
+                   const float* lnpart, int lnslots, int lnD, float lneps);
 int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqkv,
                      float scale, void* out, int ldo, int dtype, hipStream_t stream,
                      double flops);
@@ -420,7 +423,19 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     partials = gemm_emits_stats(M, Dp, dt, &e);
     if (!partials) { e.statout = nullptr; e.stat_ld = 0; }
   };
+  // partials: with VTD_LN_FUSE=1 the consumer GEMM merges them itself (gemm_launch_ln: no
+  // finalize launch, one dependent launch fewer per LayerNorm); default: the finalize kernel
+  // (read per call)
+  const bool ln_fuse = [] {
+    const char* v = getenv("VTD_LN_FUSE");
+    return v && atoi(v) != 0;
+  }();
+  bool ln_pending = false;
   auto row_stats = [&]() -> int {
+    if (partials && ln_fuse) {
+      ln_pending = true;
+      return VTD_OK;
+    }
     return partials ? ln_stats_finalize_launch(pstat, R, nslot, D, 1e-3f, stat, st)
                     : ln_stats_launch(x, rdt, R, D, Dp, 1e-3f, stat, st);
   };
@@ -440,7 +455,13 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   // against the MX-fp8 weights (W [Np][K8], S [K8/128][Np][4])
   auto enc_gemm = [&](int Np, int K, const void* a, const void* W, const uint8_t* S,
                       const vtd_epilogue* e, double flops) -> int {
-    if (!fp8) return gemm_launch(M, Np, K, a, K, W, K, dt, e, st, flops);
+    if (!fp8) {
+      if (ln_pending && e->lnstat) {
+        ln_pending = false;
+        return gemm_launch_ln(M, Np, K, a, K, W, K, dt, e, st, flops, pstat, nslot, D, 1e-3f);
+      }
+      return gemm_launch(M, Np, K, a, K, W, K, dt, e, st, flops);
+    }
     const int K8 = k8_of(K);
     int r = quantize_mx8_launch(a, VTD_BF16, R, K, K, K8, q8, K8, s8, P.s8_rows, st);
     if (r) return r;
