@@ -519,9 +519,7 @@ __device__ __forceinline__ int swz_v(int row) { return ((row >> 1) & 1) << 2; }
 template <int NB>   // key blocks of 32: N in (32 (NB - 1), 32 NB]
 __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
     const bf16_t* __restrict__ qkv, int npairs, int N, int heads, int ldqkv, float scale_log2,
-    bf16_t* __restrict__ out, int ldo, int diag) {
-  // diag (timing diagnostics only, wrong outputs): bit 0 = no DMA after the first pair (compute
-  // on stale slots), bit 1 = no compute (DMA, restage and stores only)
+    bf16_t* __restrict__ out, int ldo) {
   constexpr int DKP = 64;
   typedef __attribute__((address_space(3))) void lds_void_t;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -532,7 +530,7 @@ __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
   char* const qarea = smem + 2 * SLOT;
   const int inner = heads * DKP;
   const int q0 = wave * 32;
-  const bool active = q0 < N && !(diag & 2);
+  const bool active = q0 < N;
   const int G = gridDim.x;
   const int ngroups = NR >> 3;                   // 8-row groups per matrix
   const int lrow = lane >> 3, lchunk = lane & 7;
@@ -576,7 +574,7 @@ __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
                                                    (((st * 2 + half) ^ swz_kq(row)) << 4));
     }
     const int pn = p + G;
-    const bool fetch = pn < npairs && !(diag & 1);
+    const bool fetch = pn < npairs;
     if (fetch) {
       char* const kn = smem + ((it + 1) & 1) * SLOT;
       issue(pn, 1, kn);
@@ -723,34 +721,27 @@ int launch_bf16_ps(const void* qkv, int B, int N, int heads, int ldqkv, float sc
                    int ldo, hipStream_t stream) {
   const int NR = (N + 31) & ~31;
   const int lds = 5 * NR * 128;
-  static int ncu = 0;
-  static bool attr_set = false;
-  if (!attr_set) {
+  static std::once_flag once[kMaxDevices];
+  once_per_device(once, [] {
     for (const void* f : {reinterpret_cast<const void*>(&attention_bf16_ps_kernel<5>),
                           reinterpret_cast<const void*>(&attention_bf16_ps_kernel<6>),
                           reinterpret_cast<const void*>(&attention_bf16_ps_kernel<7>),
                           reinterpret_cast<const void*>(&attention_bf16_ps_kernel<8>)})
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 5 * 256 * 128);
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu <= 0) ncu = 256;
-    attr_set = true;
-  }
+  });
+  const int ncu = device_cu_count();
   const int npairs = B * heads;
   // workgroups: one per CU (VTD_ATTN_GRID overrides, read per call: A/B of co-running
   // the two micro-batch streams' attention on disjoint halves of the chip)
   const char* genv = getenv("VTD_ATTN_GRID");
   const int grid = std::min(npairs, genv && atoi(genv) > 0 ? atoi(genv) : ncu);
-  const char* denv = getenv("VTD_ATTN_DIAG");
-  const int diag = denv ? atoi(denv) : 0;
   auto* kern = NR == 160 ? attention_bf16_ps_kernel<5>
                : NR == 192 ? attention_bf16_ps_kernel<6>
                : NR == 224 ? attention_bf16_ps_kernel<7>
                            : attention_bf16_ps_kernel<8>;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, stream, static_cast<const bf16_t*>(qkv),
                      npairs, N, heads, ldqkv, scale * 1.4426950408889634f,
-                     static_cast<bf16_t*>(out), ldo, diag);
+                     static_cast<bf16_t*>(out), ldo);
   VTD_LAUNCH_CHECK("attention_bf16_ps");
   return VTD_OK;
 }
@@ -762,13 +753,12 @@ int launch_bf16_v2(const void* qkv, int B, int N, int heads, int ldqkv, float sc
   using C = AttnBf16Cfg<DKP>;
   const int nq = (N + 31) / 32;
   dim3 grid((nq + NWG - 1) / NWG, heads, B);
-  static bool attr_set = false;
-  if (!attr_set) {
+  static std::once_flag once[kMaxDevices];
+  once_per_device(once, [] {
     (void)hipFuncSetAttribute(
         reinterpret_cast<const void*>(&attention_bf16_kernel<DKP, NWG, MX8>),
         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * C::BUF);
-    attr_set = true;
-  }
+  });
   hipLaunchKernelGGL((attention_bf16_kernel<DKP, NWG, MX8>), grid, dim3(64 * NWG), 2 * C::BUF,
                      stream, static_cast<const bf16_t*>(qkv), N, heads, ldqkv,
                      scale * 1.4426950408889634f, static_cast<bf16_t*>(out), ldo, s8, s_rows);
@@ -783,12 +773,11 @@ int launch(const void* qkv, int B, int N, int heads, int ldqkv, float scale, voi
   const int nq = (N + 31) / 32;
   const int nw = nq <= 8 ? nq : 8;
   dim3 grid((nq + nw - 1) / nw, heads, B);
-  static bool attr_set = false;
-  if (!attr_set) {
+  static std::once_flag once[kMaxDevices];
+  once_per_device(once, [] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_kernel<T, DKP>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
-    attr_set = true;
-  }
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+  });
   const float scale_log2 = scale * 1.4426950408889634f;
   hipLaunchKernelGGL((attention_kernel<T, DKP>), grid, dim3(64 * nw), C::LDS, stream,
                      static_cast<const T*>(qkv), N, heads, ldqkv, scale_log2,

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
 #include <string>
 
 #include "../../include/vtd.h"
@@ -33,6 +34,17 @@ int fail(int code, const std::string& msg);
   } while (0)
 
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+// Per-device lazily initialised launch state (kernel attributes, CU counts): one
+// std::once_flag per device makes the first use on each device thread-safe, and the
+// calls stay re-entrant across host threads.
+constexpr int kMaxDevices = 64;
+int current_device();              // hipGetDevice, clamped to [0, kMaxDevices)
+int device_cu_count();             // compute units of the current device (cached)
+template <class F>
+void once_per_device(std::once_flag (&flags)[kMaxDevices], F&& fn) {
+  std::call_once(flags[current_device()], fn);
+}
 
 // profiling hooks (vtd_profile.cpp); no-ops unless enabled
 enum ProfClass { PROF_GEMM = 0, PROF_ATTN = 1, PROF_LN = 2, PROF_PATCH = 3, PROF_OTHER = 4 };

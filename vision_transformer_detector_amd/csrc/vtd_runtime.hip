@@ -49,6 +49,26 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+// ------------------------------------------------------------------ devices
+int current_device() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) dev = 0;
+  return dev;
+}
+int device_cu_count() {
+  static std::once_flag once[kMaxDevices];
+  static int ncu[kMaxDevices];
+  const int dev = current_device();
+  std::call_once(once[dev], [dev] {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+    ncu[dev] = n;
+  });
+  return ncu[dev];
+}
+
 // ------------------------------------------------------------------ profiling
 namespace {
 struct ProfRecord { int cls; int ev0, ev1; double flops; };
@@ -423,19 +443,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     partials = gemm_emits_stats(M, Dp, dt, &e);
     if (!partials) { e.statout = nullptr; e.stat_ld = 0; }
   };
-  // partials: with VTD_LN_FUSE=1 the consumer GEMM merges them itself (gemm_launch_ln: no
-  // finalize launch, one dependent launch fewer per LayerNorm); default: the finalize kernel
-  // (read per call)
-  const bool ln_fuse = [] {
-    const char* v = getenv("VTD_LN_FUSE");
-    return v && atoi(v) != 0;
-  }();
-  bool ln_pending = false;
   auto row_stats = [&]() -> int {
-    if (partials && ln_fuse) {
-      ln_pending = true;
-      return VTD_OK;
-    }
     return partials ? ln_stats_finalize_launch(pstat, R, nslot, D, 1e-3f, stat, st)
                     : ln_stats_launch(x, rdt, R, D, Dp, 1e-3f, stat, st);
   };
@@ -455,13 +463,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   // against the MX-fp8 weights (W [Np][K8], S [K8/128][Np][4])
   auto enc_gemm = [&](int Np, int K, const void* a, const void* W, const uint8_t* S,
                       const vtd_epilogue* e, double flops) -> int {
-    if (!fp8) {
-      if (ln_pending && e->lnstat) {
-        ln_pending = false;
-        return gemm_launch_ln(M, Np, K, a, K, W, K, dt, e, st, flops, pstat, nslot, D, 1e-3f);
-      }
-      return gemm_launch(M, Np, K, a, K, W, K, dt, e, st, flops);
-    }
+    if (!fp8) return gemm_launch(M, Np, K, a, K, W, K, dt, e, st, flops);
     const int K8 = k8_of(K);
     int r = quantize_mx8_launch(a, VTD_BF16, R, K, K, K8, q8, K8, s8, P.s8_rows, st);
     if (r) return r;
