@@ -12,7 +12,9 @@
 One step = one forward of B images per rank (images already resident in HBM) + the
 device-side decode (transform_predictions) + the RCCL all-gather of the (B, 17, 6)
 detections over all ranks (the path's only exchange; skipped at N = 1).
-Prints ONE JSON line on rank 0.
+Prints ONE JSON line on rank 0; after the timed region every rank checks that the gathered
+detections hold its own shard bit for bit (`gather_ok`) and reports its own time
+(`rank_ms_min` / `rank_ms_max` over ranks).
 """
 import argparse
 import json
@@ -107,26 +109,48 @@ def gemm_alg_bytes(kw, dims, b, rb=2):
     return tot / len(g)
 
 
-def cpu_baseline(model, kw, shape, seconds=12.0):
-    """The oracle's fp32 torch-CPU restatement (oracle/vtd_torch_cpu.py) of the same
-    graph on the host cores: the reference's TF-CPU path cannot run in this pipeline
-    (TF/Keras/tfa absent), so this is the "port" baseline."""
+def cpu_baseline(model, kw, shape, preset):
+    """The oracle's fp32 torch-CPU restatement (oracle/vtd_torch_cpu.py) of the same graph on
+    the host cores: the reference's TF-CPU path cannot run in this pipeline (TF/Keras/tfa
+    absent), so this is the "port" baseline.  SURVEY.md §8(d)'s plan: C1 (the
+    reference default) and C2 (ViT-B/16 @224), batch 1 and 8, median of 5 forwards after 1
+    warm-up, torch's host threads (OMP_NUM_THREADS).  `value` = the bench preset's batch-8 median when it is one of
+    the two (else C2's)."""
+    import statistics
+    import numpy as np
+    import vision_transformer_detector_amd as vtd
+    from oracle import vtd_numpy as ref
     from oracle.vtd_torch_cpu import TorchCpuDetector
-    threads = torch.get_num_threads()
-    det = TorchCpuDetector(model.get_weight_dict(), **kw)
-    b = 4
-    x = letterbox_images(b, shape, torch.Generator().manual_seed(7), "cpu")
-    det(x)                                   # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        det(x)
-        n += 1
-        el = time.perf_counter() - t0
-        if el > seconds or n >= 50:
-            break
-    return {"value": b * n / el, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} forwards x batch {b} ({b * n} images, {el:.1f} s) of the same "
-                      f"preset on the fp32 torch-CPU restatement, {threads} threads"}
+    threads = torch.get_num_threads()      # OMP_NUM_THREADS: the host-core share of this job
+    cases = {}
+    t_all = time.perf_counter()
+    for name in ("c1", "vit_b16_224"):
+        pkw = dict(vtd.presets.PRESETS[name])
+        if name == preset:
+            det = TorchCpuDetector(model.get_weight_dict(), **kw)
+            pshape = shape
+        else:
+            det = TorchCpuDetector(ref.init_weights(seed=0, **pkw), **pkw)
+            pshape = tuple(ref.resolve_kwargs(**pkw)["input_shape"])
+        for b in (1, 8):
+            x = letterbox_images(b, pshape, torch.Generator().manual_seed(7), "cpu")
+            det(x)                                           # warm-up
+            ts = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                det(x)
+                ts.append(time.perf_counter() - t0)
+            med = statistics.median(ts)
+            cases[f"{name}_b{b}"] = {"images_per_s": round(b / med, 3),
+                                     "median_s": round(med, 4)}
+    key = f"{preset if preset in ('c1', 'vit_b16_224') else 'vit_b16_224'}_b8"
+    return {"value": cases[key]["images_per_s"], "unit": "images/s", "cores": threads,
+            "kind": "port",
+            "sample": f"median of 5 forwards after 1 warm-up, batch 1 and 8, C1 (608x608 "
+                      f"default) and C2 (ViT-B/16 @224), fp32 torch-CPU restatement, "
+                      f"{threads} threads, {time.perf_counter() - t_all:.1f} s in all; "
+                      f"value = {key}",
+            "cases": cases}
 
 
 def _free_port():
@@ -167,6 +191,32 @@ def launch_ranks(n):
     return code
 
 
+def rank_spread(elapsed, world, device):
+    """Every rank's own timed-region length -> (min, max) over ranks (max = the job's)."""
+    if world == 1:
+        return {"min_s": elapsed, "max_s": elapsed}
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    ts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(ts, t)
+    v = [float(x.item()) for x in ts]
+    return {"min_s": min(v), "max_s": max(v)}
+
+
+def check_gather(dets, world, rank, B, device):
+    """Outside the timed region: one more all-gather of this rank's detections; every rank
+    checks that the gathered (world*B, 17, 6) holds its own shard bit for bit at its offset
+    and that every shard is finite.  Returns the AND over ranks."""
+    from vision_transformer_detector_amd.distributed import all_gather_detections
+    g = all_gather_detections(dets, world * B) if world > 1 else dets
+    ok = (g.shape[0] == world * B and torch.equal(g[rank * B:(rank + 1) * B], dets)
+          and bool(torch.isfinite(g).all()))
+    if world > 1:
+        f = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        ok = bool(f.item())
+    return ok
+
+
 def dry_run(args, world, rank):
     """CPU rehearsal of the multi-rank path (gloo): the launcher, the rendezvous, the
     barrier / max-over-ranks timing and the all-gather of (B, 17, 6) detections, without
@@ -186,12 +236,11 @@ def dry_run(args, world, rank):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    spread = rank_spread(elapsed, world, "cpu")
+    elapsed = spread["max_s"]
     ranks_ok = out.shape[0] == world * B and all(
         bool((out[r * B:(r + 1) * B] == r).all()) for r in range(world))
+    gather_ok = check_gather(dets, world, rank, B, "cpu")
     if rank == 0:
         print(json.dumps({
             "metric": "dry-run: all-gather of detections only (no GPU forward)",
@@ -200,6 +249,9 @@ def dry_run(args, world, rank):
             "ms_per_step": round(1e3 * elapsed / max(1, args.steps), 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic", "gather_rank_order_ok": ranks_ok,
+            "gather_ok": gather_ok,
+            "rank_ms_min": round(1e3 * spread["min_s"] / max(1, args.steps), 3),
+            "rank_ms_max": round(1e3 * spread["max_s"] / max(1, args.steps), 3),
             "config": {"workload": "dry-run (gloo, CPU)", "per_gpu_batch": B,
                        "global_batch": world * B, "parallelism": f"dp{world}"}}), flush=True)
     if world > 1:
@@ -223,7 +275,6 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streams", type=int, default=2,
                     help="vtd_forward micro-batch streams (VTD_STREAMS; 1 = one stream)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--graph", type=int, default=0,
                     help="1: the forward of a step is one HIP-graph replay (captured once after "
                          "warm-up); 0: eager vtd_forward calls")
@@ -306,10 +357,12 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    spread = rank_spread(elapsed, world, dev)
+    elapsed = spread["max_s"]
+    # correctness evidence of the timed path (outside the timed region): this rank's
+    # detections, gathered over all ranks, sit bit for bit at its shard offset, all finite
+    _, dets_chk = model.detect(images)
+    gather_ok = check_gather(dets_chk, world, rank, B, dev)
 
     # ---- per-kernel timing: hipEvents recorded around every launch of vtd_forward on
     # the stream it launches on, over K more steps of the same workload.  Profiling runs
@@ -342,8 +395,13 @@ def main():
     peak = PEAK_TFLOPS[args.dtype]
     g = kernels["gemm"]
     gemm_tf = g["tflops"]
+    headline = args.preset == "vit_b16_224" and B == 256 and args.dtype == "bf16"
+    metric = ("images/sec ViT-B/16 detector fwd, batch 256, 1/2/4/8 MI355X; MFMA util %"
+              if headline else
+              f"images/sec {args.preset} detector fwd, batch {B} per GPU, {args.dtype}, "
+              f"{world} MI355X; MFMA util %")
     out = {
-        "metric": "images/sec ViT-B/16 detector fwd, batch 256, 1/2/4/8 MI355X; MFMA util %",
+        "metric": metric,
         "value": round(img_s, 2),
         "unit": "images/s",
         "n_gpus": world,
@@ -356,8 +414,9 @@ def main():
         "dtype": args.dtype,
         "data": "synthetic (U(-1,1) NHWC letterboxed images generated on device; "
                 "random Keras-default-init weights)",
-        "config": {"workload": f"{args.preset} detector forward + decode + all-gather of "
-                               f"detections", "per_gpu_batch": B, "global_batch": world * B,
+        "config": {"workload": f"{args.preset} detector forward + decode" +
+                               (" + RCCL all-gather of detections" if world > 1 else ""),
+                   "per_gpu_batch": B, "global_batch": world * B,
                    "input_shape": list(shape), "tokens": model.dims.tokens,
                    "parallelism": f"dp{world}", "streams_per_gpu": args.streams,
                    "hip_graph": bool(args.graph)},
@@ -381,9 +440,12 @@ def main():
         "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv)
                         for kk, vv in v.items()} for k, v in kernels.items()},
         "profiled_ms_per_step": round(1e3 * prof_elapsed / args.steps, 3),
+        "gather_ok": gather_ok,
+        "rank_ms_min": round(1e3 * spread["min_s"] / args.steps, 3),
+        "rank_ms_max": round(1e3 * spread["max_s"] / args.steps, 3),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(model, kw, shape, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(model, kw, shape, args.preset)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

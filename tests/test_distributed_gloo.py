@@ -120,6 +120,9 @@ def test_bench_launches_ranks_itself(world):
     out = json.loads(lines[0])
     assert out["n_gpus"] == world and out["config"]["global_batch"] == 5 * world
     assert out["gather_rank_order_ok"] is True
+    # correctness evidence of the N > 1 line: each rank finds its own shard in the gather
+    assert out["gather_ok"] is True
+    assert 0 <= out["rank_ms_min"] <= out["rank_ms_max"]
 
 
 def test_bench_rejects_gpus_world_mismatch():
