@@ -140,6 +140,19 @@ int main() {
     for (size_t i = 2; i < bad.size(); i += 3) bad[i] ^= 0x5A;
     (void)vtd_jpeg_info(bad.data(), bad.size(), &h, &w, &c);
     CHECK(vtd_jpeg_info(nullptr, 10, &h, &w, &c) == VTD_ERR_INVALID_ARG);
+    // a DRI / SOS segment with no payload that ends the buffer (exactly sized copies, so any
+    // read of a payload byte is a heap overflow ASan reports)
+    size_t sos = 0;
+    for (size_t i = 0; i + 1 < sizeof(kJpeg); ++i)
+      if (kJpeg[i] == 0xFF && kJpeg[i + 1] == 0xDA) { sos = i; break; }
+    CHECK(sos > 0);
+    for (uint8_t mk : {uint8_t(0xDD), uint8_t(0xDA)}) {
+      std::vector<uint8_t> f(kJpeg, kJpeg + sos);
+      const uint8_t seg[4] = {0xFF, mk, 0x00, 0x02};
+      f.insert(f.end(), seg, seg + 4);
+      std::vector<uint8_t> exact(f.begin(), f.end());
+      CHECK(vtd_jpeg_info(exact.data(), exact.size(), &h, &w, &c) != VTD_OK);
+    }
   }
   // profiling state (host only)
   CHECK(vtd_profile_reset() == VTD_OK);

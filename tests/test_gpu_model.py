@@ -248,6 +248,22 @@ def test_bf16_with_f32_residual_stream_env(cuda):
     assert r.returncode == 0, r.stdout + r.stderr[-3000:]
 
 
+def test_dropout_model_is_the_same_forward(vtd, cuda):
+    """A model built with dropout=0.1 (Dropout layers + MHA dropout in the reference,
+    vtd.py:359-369, 404-405, 485-486) has the same weight names and, at inference, the same
+    logits as dropout=None; it loads the same Keras HDF5 file."""
+    import sys
+    sys.path.insert(0, GOLD)
+    from make_keras_h5 import TINY
+    x = torch.from_numpy(V.synthetic_images(2, TINY["input_shape"], seed=5)).to(cuda)
+    m0 = vtd.create_vision_transformer_detector(**TINY, dtype="float32")
+    m1 = vtd.create_vision_transformer_detector(**TINY, dropout=0.1, dtype="float32")
+    m1.load_weights(os.path.join(GOLD, "tiny_keras.h5"))
+    m0.load_weights(os.path.join(GOLD, "tiny_keras.h5"))
+    assert list(m0.get_weight_dict()) == list(m1.get_weight_dict())
+    assert torch.equal(m0(x, training=False), m1(x, training=False))
+
+
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
 def test_load_weights_from_keras_hdf5(vtd, cuda, dtype):
     """Model.load_weights('*.keras' / '*.h5'): the Keras 2.9 HDF5 layout of the reference's

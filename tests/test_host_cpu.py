@@ -173,15 +173,21 @@ def test_model_requires_a_hip_device():
                                                embedding_dim=8, device="cpu")
 
 
-def test_dropout_must_be_none():
+def test_dropout_rates_and_training_flag():
+    """dropout is the identity at inference (vtd.py:369, 405, 486 run with the call's
+    training flag): any rate in [0, 1) is accepted (the GPU test checks the logits); a rate
+    outside it, or a build-time training=True with dropout on, is refused before any
+    device work."""
     import vision_transformer_detector_amd as vtd
-    with pytest.raises(ValueError):
-        vtd.create_vision_transformer_detector(dropout=0.1)
+    with pytest.raises(ValueError, match="dropout rate"):
+        vtd.create_vision_transformer_detector(dropout=1.5)
+    with pytest.raises(ValueError, match="training=True"):
+        vtd.create_vision_transformer_detector(dropout=0.1, training=True)
 
 
-def test_pp3_lds_swizzle_conflict_free():
-    """The pp3 GEMM's 64-B-row LDS swizzle serves every ds_read_b128 lane group of its
-    plain and permuted fragment reads without bank conflicts (tools/swizzle_check.py)."""
+def test_gemm_lds_swizzle_conflict_free():
+    """The 256-tile GEMMs' 128-B-row LDS swizzles serve every ds_read_b128 lane group of
+    their plain and permuted fragment reads without bank conflicts (tools/swizzle_check.py)."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -87,6 +87,36 @@ def test_unsupported_flavours_name_the_reason(L):
     assert rc != 0 and b"image 1" in L.lib.vtd_last_error()
 
 
+def _with_sof_sampling(f, comp0):
+    """A copy of baseline JPEG f with component 0's sampling byte of the SOF0 replaced."""
+    i = f.index(b"\xff\xc0")
+    b = bytearray(f)
+    b[i + 2 + 2 + 6 + 1] = comp0         # marker, length, P/Y/X/Nf, then C1 id, H1V1
+    return bytes(b)
+
+
+def test_440_subsampling_is_refused(L):
+    """4:4:0 (luma 1 x 2, chroma 1 x 1) would need libjpeg-turbo's h1v2 upsampling, which the
+    colour pass does not implement: the header walk refuses it by name."""
+    f = _with_sof_sampling(_jpeg(32, 32, quality=80, subsampling=0), 0x12)
+    rc, _ = _info(L, f)
+    assert rc != 0 and b"4:4:0" in L.lib.vtd_last_error()
+
+
+def _segment(marker, payload):
+    return b"\xff" + bytes([marker]) + (len(payload) + 2).to_bytes(2, "big") + payload
+
+
+@pytest.mark.parametrize("marker", [0xDD, 0xDA])
+def test_short_dri_sos_at_the_end_of_the_file(L, marker):
+    """A DRI / SOS segment whose declared length leaves no payload, placed so that the
+    segment ends the buffer: refused before any payload byte is read (ASan host check too)."""
+    f = _jpeg(16, 16, quality=80)
+    head = f[:f.index(b"\xff\xda")]    # everything before the scan
+    rc, _ = _info(L, head + _segment(marker, b""))
+    assert rc != 0 and b"truncated" in L.lib.vtd_last_error()
+
+
 @pytest.mark.parametrize("data", [b"", b"\x00\x01not a jpeg", b"\xff\xd8", b"\xff\xd8\xff\xd9",
                                   b"\xff\xd8\xff\xdb\x00\x43\x00"])
 def test_malformed_input_fails_cleanly(L, data):

@@ -113,3 +113,28 @@ def test_errors(tmp_path):
     w.save(str(p))
     with pytest.raises(H5Error, match="layer_names"):
         read_keras_weights(str(p))
+
+
+def _self_continuing_file(path):
+    """A minimal superblock-v0 file whose root object header (v1) holds only a continuation
+    message pointing back at its own message block: a crafted header chain that loops."""
+    import struct
+    A = 96                                        # root object header address
+    sb = (b"\x89HDF\r\n\x1a\n" + bytes([0, 0, 0, 0, 0, 8, 8, 0]) + struct.pack("<HHI", 4, 16, 0)
+          + struct.pack("<QQQQ", 0, 0xFFFFFFFFFFFFFFFF, 4096, 0xFFFFFFFFFFFFFFFF)
+          + struct.pack("<QQII16x", 0, A, 0, 0))
+    msg = struct.pack("<HHB3x", 0x10, 16, 0) + struct.pack("<QQ", A + 16, 24)
+    hdr = struct.pack("<BBHII4x", 1, 0, 1, 1, len(msg)) + msg
+    buf = bytearray(4096)
+    buf[:len(sb)] = sb
+    buf[A:A + len(hdr)] = hdr
+    path.write_bytes(bytes(buf))
+
+
+def test_continuation_loop_is_refused(tmp_path):
+    """A header continuation chain that loops back on itself raises H5Error instead of
+    walking forever (load_weights of an untrusted file must return)."""
+    p = tmp_path / "loop.h5"
+    _self_continuing_file(p)
+    with pytest.raises(H5Error, match="continuation"):
+        H5File(str(p))

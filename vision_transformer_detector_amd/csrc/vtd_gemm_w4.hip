@@ -93,6 +93,12 @@ __device__ __forceinline__ void w4_sources(W4Src& s, const bf16_t* A, int lda, i
   }
 }
 
+#ifndef VTD_DIAG
+#define VTD_DIAG 0
+#endif
+// DG (VTD_DIAG builds only; timing diagnostics, WRONG outputs): bit 0 = no DMA after the
+// prologue (every K-step reads stale stages), bit 1 = every DMA re-fetches K-tile 0 (the
+// same instruction stream from L2-resident lines)
 __device__ __forceinline__ void w4_dma(char* stage, const W4Src& s, int wave, int kt, int j) {
   char* da = stage + wave * 64 * 128 + j * 1024;
   __builtin_amdgcn_raw_ptr_buffer_load_lds(s.ra, (w4_lds_t*)da, 16, s.offa[j], kt * 128, 0, 0);
@@ -137,8 +143,8 @@ __device__ __forceinline__ void w4_mfma_row(f32x4 (&acc)[8][8], const W4Frag& f,
 
 // One K-step (see the file comment).  PF: tile kt + 2 exists (DMA it); NN: tile kt + 1
 // exists (read its first fragments).  Compile-time flags: no branch inside the step.
-template <bool PF, bool NN>
-__device__ __forceinline__ void w4_kstep(f32x4 (&acc)[8][8], W4Frag& f0, W4Frag& f1, char* smem,
+template <bool PF, bool NN, int DG>
+__device__ __forceinline__ void w4_kstep0(f32x4 (&acc)[8][8], W4Frag& f0, W4Frag& f1, char* smem,
                                          const W4Src& src, int kt, int wave, int aoff0,
                                          int aoff1, int b00, int b01, int b10, int b11) {
   char* st = smem + (kt & 1) * W4_STAGE;
@@ -158,9 +164,9 @@ __device__ __forceinline__ void w4_kstep(f32x4 (&acc)[8][8], W4Frag& f0, W4Frag&
   // ---- the rest of F0, DMA of tile kt + 2 into stage st (4 instructions per 8 MFMAs)
 #pragma unroll
   for (int i = 2; i < 8; ++i) {
-    if (PF && i < 6) {
-      w4_dma(st, src, wave, kt + 2, 2 * (i - 2));
-      w4_dma(st, src, wave, kt + 2, 2 * (i - 2) + 1);
+    if (PF && !(DG & 1) && i < 6) {
+      w4_dma(st, src, wave, (DG & 2) ? 0 : kt + 2, 2 * (i - 2));
+      w4_dma(st, src, wave, (DG & 2) ? 0 : kt + 2, 2 * (i - 2) + 1);
     }
     w4_mfma_row(acc, f0, i);
     w4_fence();
@@ -179,6 +185,36 @@ __device__ __forceinline__ void w4_kstep(f32x4 (&acc)[8][8], W4Frag& f0, W4Frag&
   }
 }
 
+// Schedule 1: one barrier per K-step.  F1(kt) is read during F0(kt)'s MFMAs; the barrier
+// then retires both every wave's reads of stage st (WAR for tile kt + 2's DMA, issued during
+// F1's MFMAs) and tile kt + 1's DMA (RAW for F0(kt + 1)'s reads, also during F1's MFMAs).
+template <bool PF, bool NN, int DG>
+__device__ __forceinline__ void w4_kstep1(f32x4 (&acc)[8][8], W4Frag& f0, W4Frag& f1, char* smem,
+                                          const W4Src& src, int kt, int wave, int aoff0,
+                                          int aoff1, int b00, int b01, int b10, int b11) {
+  char* st = smem + (kt & 1) * W4_STAGE;
+  char* nx = smem + ((kt + 1) & 1) * W4_STAGE;
+  w4_fence();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    w4_read2(f1, st, i, aoff1, b10, b11);
+    w4_mfma_row(acc, f0, i);
+    w4_fence();
+  }
+  w4_fence();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile kt + 1 (the only DMA in flight)
+  w4_barrier();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (PF && !(DG & 1)) w4_dma(st, src, wave, (DG & 2) ? 0 : kt + 2, i);
+    if (NN) w4_read2(f0, nx, i, aoff0, b00, b01);
+    w4_mfma_row(acc, f1, i);
+    w4_fence();
+  }
+}
+
+template <int SCHED, int DG>
 __device__ __forceinline__ void w4_mainloop(f32x4 (&acc)[8][8], char* smem, const W4Src& src,
                                             int nk, int wave, int wm, int wn, int lane) {
   const int fr = lane & 15, fg = lane >> 4;
@@ -203,13 +239,20 @@ __device__ __forceinline__ void w4_mainloop(f32x4 (&acc)[8][8], char* smem, cons
 #pragma unroll
   for (int g = 0; g < 8; ++g) w4_read2(f0, smem, g, aoff0, b00, b01);
   int kt = 0;
-  for (; kt + 2 < nk; ++kt)
-    w4_kstep<true, true>(acc, f0, f1, smem, src, kt, wave, aoff0, aoff1, b00, b01, b10, b11);
+#define VTD_W4_STEP(PF, NN)                                                                    \
+  if constexpr (SCHED == 0)                                                                    \
+    w4_kstep0<PF, NN, DG>(acc, f0, f1, smem, src, kt, wave, aoff0, aoff1, b00, b01, b10, b11); \
+  else                                                                                         \
+    w4_kstep1<PF, NN, DG>(acc, f0, f1, smem, src, kt, wave, aoff0, aoff1, b00, b01, b10, b11);
+  for (; kt + 2 < nk; ++kt) {
+    VTD_W4_STEP(true, true)
+  }
   if (kt + 1 < nk) {
-    w4_kstep<false, true>(acc, f0, f1, smem, src, kt, wave, aoff0, aoff1, b00, b01, b10, b11);
+    VTD_W4_STEP(false, true)
     ++kt;
   }
-  w4_kstep<false, false>(acc, f0, f1, smem, src, kt, wave, aoff0, aoff1, b00, b01, b10, b11);
+  VTD_W4_STEP(false, false)
+#undef VTD_W4_STEP
 }
 
 // ---- epilogues ---------------------------------------------------------------------
@@ -315,7 +358,7 @@ __device__ __forceinline__ void w4_epilogue_generic(const f32x4 (&acc)[8][8], fl
   }
 }
 
-template <int EPI>
+template <int EPI, int SCHED = 1, int DG = 0>
 __global__ __launch_bounds__(W4_T, 1) void gemm_tn_bf16_w4_kernel(
     int M, int N, int K, const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ Bt,
     int ldb, int tiles_m, int tiles_n, EpiArgs e) {
@@ -344,7 +387,7 @@ __global__ __launch_bounds__(W4_T, 1) void gemm_tn_bf16_w4_kernel(
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  w4_mainloop(acc, smem, src, K / 64, wave, wm, wn, lane);
+  w4_mainloop<SCHED, DG>(acc, smem, src, K / 64, wave, wm, wn, lane);
   const int m_base = m0 + wm * 128, n_base = n0 + wn * 128;
   if constexpr (EPI != EPI_GENERIC) {
     if (m0 + W4_TILE <= M && n0 + W4_TILE <= N) {
@@ -356,11 +399,23 @@ __global__ __launch_bounds__(W4_T, 1) void gemm_tn_bf16_w4_kernel(
                       m_base, n_base, e);
 }
 
-template <int C>
+template <int C, int SCHED, int DG = 0>
 void w4_launch(dim3 g, hipStream_t stream, int M, int N, int K, const bf16_t* A, int lda,
                const bf16_t* Bt, int ldb, int tiles_m, int tiles_n, const EpiArgs& e) {
-  hipLaunchKernelGGL((gemm_tn_bf16_w4_kernel<C>), g, dim3(W4_T), W4_LDS, stream, M, N, K, A, lda,
-                     Bt, ldb, tiles_m, tiles_n, e);
+  static std::once_flag once[kMaxDevices];
+  once_per_device(once, [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_bf16_w4_kernel<C, SCHED, DG>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, W4_LDS);
+  });
+  hipLaunchKernelGGL((gemm_tn_bf16_w4_kernel<C, SCHED, DG>), g, dim3(W4_T), W4_LDS, stream, M, N,
+                     K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
+}
+
+// K-loop schedule (VTD_W4_SCHED, read per call: A/B in one process; both exact):
+// 1 = one barrier per K-step (default), 0 = two barriers per K-step
+int w4_sched() {
+  const char* v = getenv("VTD_W4_SCHED");
+  return v && atoi(v) == 0 ? 0 : 1;
 }
 
 }  // namespace
@@ -369,19 +424,6 @@ void w4_launch(dim3 g, hipStream_t stream, int M, int N, int K, const bf16_t* A,
 // LayerNorm partials into epi->lnstat).  Returns false when it does not apply.
 bool gemm_w4_launch(int M, int N, int K, const bf16_t* A, int lda, const bf16_t* Bt, int ldb,
                     const vtd_epilogue* epi, int ngw, hipStream_t stream) {
-  static std::once_flag once;
-  static bool ok = true;
-  std::call_once(once, [] {
-#define VTD_W4_FN(C) reinterpret_cast<const void*>(&gemm_tn_bf16_w4_kernel<C>),
-    const void* fns[] = {VTD_W4_FN(EPI_GENERIC) VTD_W4_FN(0) VTD_W4_FN(1) VTD_W4_FN(2)
-                         VTD_W4_FN(4) VTD_W4_FN(5) VTD_W4_FN(6) VTD_W4_FN(8) VTD_W4_FN(9)
-                         VTD_W4_FN(10) VTD_W4_FN(12) VTD_W4_FN(13) VTD_W4_FN(14)};
-#undef VTD_W4_FN
-    for (const void* f : fns)
-      if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, W4_LDS) != hipSuccess)
-        ok = false;
-  });
-  if (!ok) return false;
   EpiArgs e = make_epi_args(epi);
   e.ngw = ngw;
   auto a16 = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
@@ -392,14 +434,32 @@ bool gemm_w4_launch(int M, int N, int K, const bf16_t* A, int lda, const bf16_t*
                         : EPI_GENERIC;
   const int tiles_m = (M + W4_TILE - 1) / W4_TILE, tiles_n = (N + W4_TILE - 1) / W4_TILE;
   const dim3 g(tiles_m * tiles_n);
+#if VTD_DIAG
+  // timing diagnostics (wrong outputs), plain bf16 epilogue only: VTD_W4_DG = 1 / 2 / 3
+  if (const char* dg = getenv("VTD_W4_DG"); dg && atoi(dg) > 0 && code == 4) {
+    const int d = atoi(dg);
+    if (d == 1) w4_launch<4, 1, 1>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
+    else if (d == 2) w4_launch<4, 1, 2>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
+    else w4_launch<4, 0, 1>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
+    return true;
+  }
+#endif
+  const int sched = w4_sched();
   switch (code) {
-#define VTD_W4_CASE(C) \
-  case C: w4_launch<C>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e); break;
+#define VTD_W4_CASE(C)                                                                        \
+  case C:                                                                                     \
+    if (sched == 1) w4_launch<C, 1>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e); \
+    else w4_launch<C, 0>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);          \
+    break;
     VTD_W4_CASE(0) VTD_W4_CASE(1) VTD_W4_CASE(2) VTD_W4_CASE(4) VTD_W4_CASE(5) VTD_W4_CASE(6)
     VTD_W4_CASE(8) VTD_W4_CASE(9) VTD_W4_CASE(10) VTD_W4_CASE(12) VTD_W4_CASE(13)
     VTD_W4_CASE(14)
 #undef VTD_W4_CASE
-    default: w4_launch<EPI_GENERIC>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
+    default:
+      if (sched == 1)
+        w4_launch<EPI_GENERIC, 1>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
+      else
+        w4_launch<EPI_GENERIC, 0>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
   }
   return true;
 }

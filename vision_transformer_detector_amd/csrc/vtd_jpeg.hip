@@ -213,17 +213,25 @@ bool parse_jpeg(const uint8_t* b, size_t n, JpegDesc& d, size_t& seg, size_t& se
           err = "jpeg: unsupported subsampling (4:4:4, 4:2:2, 4:2:0 only)";
           return false;
         }
+      // 4:4:0 (luma 1 x 2, chroma 1 x 1): the colour pass upsamples horizontally (h2v1 /
+      // h2v2) only, so libjpeg-turbo's h1v2 filter is not implemented: refuse it
+      if (d.nc > 1 && d.hmax == 1 && d.vmax == 2) {
+        err = "jpeg: unsupported subsampling 4:4:0 (4:4:4, 4:2:2, 4:2:0 only)";
+        return false;
+      }
       frame = true;
     } else if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
       err = m == 0xC2 ? "jpeg: progressive JPEG is not supported by the device decoder"
                       : "jpeg: only baseline / extended sequential Huffman JPEG is supported";
       return false;
     } else if (m == 0xDD) {                                   // DRI
+      if (len < 4) { err = "jpeg: truncated DRI segment"; return false; }
       d.restart = u16(s);
     } else if (m == 0xEE && len >= 14 && !memcmp(b + s, "Adobe", 5)) {
       d.rgb = b[s + 11] == 0 ? 1 : 0;                         // transform 0: RGB / no YCC
     } else if (m == 0xDA) {                                   // SOS
       if (!frame) { err = "jpeg: scan before frame"; return false; }
+      if (len < 3) { err = "jpeg: truncated SOS segment"; return false; }
       const int ns = b[s];
       if (ns != d.nc || len != 6 + 2 * ns) {
         err = "jpeg: only single-scan images with all components interleaved are supported";

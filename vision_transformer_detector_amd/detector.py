@@ -462,15 +462,23 @@ def create_vision_transformer_detector(
         use_mish=True,
         max_weight=10, clip_weight=True, training=None,
         *, dtype="bfloat16", device=None, seed=0) -> Model:
-    """Same kwargs and defaults as vtd.py:498-506.  `dropout` must be None or 0 (the
-    forward path is inference-only); `max_weight`/`clip_weight` are weight constraints
+    """Same kwargs and defaults as vtd.py:498-506.  `dropout` (MultiHeadAttention dropout and
+    the Dropout layers after every MLP / head activation, vtd.py:359-369, 404-405, 485-486)
+    is the identity at inference -- those layers run with the call's `training` flag, False
+    in `model(x, training=False)` / `predict` -- and Dropout has no weights, so any rate in
+    [0, 1) builds the same forward and the same weight names; only a build-time
+    `training=True` (dropout forced on in every call) is refused.  `max_weight`/`clip_weight` are weight constraints
     Keras applies only after optimizer steps (vtd.py:209-236), so they do not affect
     the forward and are accepted as no-ops.  Extra keyword-only options: `dtype`
     ('bfloat16' throughput mode, 'float32' parity mode, or 'float8': the encoder Dense
     layers in MX-fp8 on the block-scaled fp8 MFMA, everything else bfloat16), `device`,
     `seed`."""
-    if dropout not in (None, 0, 0.0):
-        raise ValueError("dropout must be None or 0 for the inference forward path")
+    if dropout is not None:
+        if not 0.0 <= float(dropout) < 1.0:
+            raise ValueError(f"dropout rate must be in [0, 1), got {dropout}")
+        if training is True and float(dropout) > 0.0:
+            raise ValueError("training=True applies dropout in every call (vtd.py:369, 405, "
+                             "486); this forward path is inference-only")
     if input_shape is None:                                       # vtd.py:550-551
         input_shape = (*Constants.MODEL_IMAGE_SIZE.value, 3)
     kw = dict(input_shape=tuple(int(v) for v in input_shape), patch_size=int(patch_size),

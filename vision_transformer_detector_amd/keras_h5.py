@@ -28,6 +28,8 @@ SIGNATURE = b"\x89HDF\r\n\x1a\n"
 UNDEF = 0xFFFFFFFFFFFFFFFF
 
 
+_MAX_HEADER_CHUNKS = 4096     # continuation chunks followed per object header
+
 class H5Error(ValueError):
     pass
 
@@ -267,8 +269,14 @@ class H5File(Group):
                 r.skip(4)
             size = r.u(1 << (flags & 3))
             todo = [(r.p, size)]
+            seen = set()
             while todo:
                 start, n = todo.pop(0)
+                # a crafted file could chain continuations in a loop: every chunk once, and
+                # a bounded number of chunks
+                if start in seen or len(seen) >= _MAX_HEADER_CHUNKS:
+                    raise H5Error("object header continuation loop / too many chunks")
+                seen.add(start)
                 p, end = start, start + n
                 while p + 4 <= end:
                     t = self.buf[p]
@@ -295,8 +303,12 @@ class H5File(Group):
         size = r.u(4)
         r.skip(4)                                 # pad to 8 (header is 16 bytes)
         todo = [(r.p, size)]
+        seen = set()
         while todo and len(out) < nmsg + 64:
             start, n = todo.pop(0)
+            if start in seen or len(seen) >= _MAX_HEADER_CHUNKS:
+                raise H5Error("object header continuation loop / too many chunks")
+            seen.add(start)
             p, end = start, start + n
             while p + 8 <= end:
                 t = int.from_bytes(self.buf[p:p + 2], "little")

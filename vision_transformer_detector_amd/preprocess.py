@@ -57,6 +57,7 @@ def get_image_tensors(images, target_height: int = MODEL_IMAGE_HEIGHT,
     offs = torch.from_numpy(offsets).to(dev)
     szs = torch.tensor(sizes, dtype=torch.int32).to(dev)
     out = torch.empty(len(flats), target_height, target_width, 3, dtype=torch.float32, device=dev)
+    _on_stream(stream, dev, pixels, offs, szs, out)
     with torch.cuda.device(dev):
         L.check(L.lib.vtd_resize_with_pad(L.ptr(pixels), L.ptr(offs), L.ptr(szs), len(flats),
                                           target_height, target_width, L.ptr(out),
@@ -92,12 +93,25 @@ def decode_jpegs(files, device="cuda", stream=None):
     pixels = torch.empty(total, dtype=torch.uint8, device=dev)
     ws = torch.empty(int(ws_bytes.value), dtype=torch.uint8, device=dev)
     offs = (ctypes.c_int64 * n)(*offsets.tolist())
+    _on_stream(stream, dev, pixels, ws)
     with torch.cuda.device(dev):
         L.check(L.lib.vtd_jpeg_decode(ptrs, lens, n, L.ptr(pixels), offs, L.ptr(ws),
                                       ws_bytes.value, L.stream_ptr(stream)), "jpeg_decode")
-    if stream is not None:                 # the allocator must not recycle the workspace
-        ws.record_stream(stream)           # before the kernels on `stream` have run
     return pixels, offsets, sizes
+
+
+def _on_stream(stream, dev, *tensors):
+    """Before launching on a caller-given `stream` that is not the current one: order it after
+    the current stream's work (the allocations and host-to-device copies of the inputs were
+    made there), and tell the caching allocator that the tensors are used on `stream`, so a
+    tensor freed at return is not handed out again before `stream`'s kernels have run."""
+    if stream is None:
+        return
+    cur = torch.cuda.current_stream(dev)
+    if stream != cur:
+        stream.wait_stream(cur)
+    for t in tensors:
+        t.record_stream(stream)
 
 
 def get_image_tensors_from_files(paths_or_bytes, target_height: int = MODEL_IMAGE_HEIGHT,
@@ -122,6 +136,7 @@ def get_image_tensors_from_files(paths_or_bytes, target_height: int = MODEL_IMAG
     offs = torch.from_numpy(offsets).to(dev)
     szs = torch.tensor(sizes, dtype=torch.int32).to(dev)
     out = torch.empty(len(files), target_height, target_width, 3, dtype=torch.float32, device=dev)
+    _on_stream(stream, dev, pixels, offs, szs, out)
     with torch.cuda.device(dev):
         L.check(L.lib.vtd_resize_with_pad(L.ptr(pixels), L.ptr(offs), L.ptr(szs), len(files),
                                           target_height, target_width, L.ptr(out),
