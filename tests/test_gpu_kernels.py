@@ -344,17 +344,19 @@ def test_gemm_bf16_256_tile_path(L, cuda, M, N, K, act, out_dtype):
     (4096, 2048, 64, 1, False),      # one K-step (no steady-state loop)
     (4096, 2048, 128, 0, False)])    # two K-steps
 def test_gemm_variants_w4_pp2(L, cuda, monkeypatch, M, N, K, act, resid):
-    """The two 256-tile bf16 kernels (VTD_GEMM_VARIANT 12 = w4, one wave per SIMD, the
-    default; 10 = pp2, 8-wave ping-pong) against fp64 and against each other (same K order
-    of the fp32 accumulation: within bf16 output rounding), with an in-place residual."""
+    """The two 256-tile bf16 kernels (VTD_GEMM_VARIANT 10 = pp2, 8-wave ping-pong, the
+    default; 12 = w4, one wave per SIMD, persistent; VTD_W4_SCHED 1 / 2) against fp64 and
+    against each other (same K order of the fp32 accumulation: within bf16 output rounding),
+    with an in-place residual."""
     g = torch.Generator(device=cuda).manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
     Bt = (torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
     bias = torch.randn(N, generator=g, device=cuda)
     x0 = (4 * torch.randn(M, N, generator=g, device=cuda)).to(torch.bfloat16)
     outs = {}
-    for v in ("10", "12"):
-        monkeypatch.setenv("VTD_GEMM_VARIANT", v)
+    for v in ("10", "12", "12s2"):
+        monkeypatch.setenv("VTD_GEMM_VARIANT", v[:2])
+        monkeypatch.setenv("VTD_W4_SCHED", "2" if v.endswith("s2") else "1")
         x = x0.clone()
         _gemm(L, A, Bt, L.BF16, bias=bias, act=act, resid=x if resid else None, out=x,
               out_dtype=1)
@@ -362,18 +364,20 @@ def test_gemm_variants_w4_pp2(L, cuda, monkeypatch, M, N, K, act, resid):
     ref64 = _np_act(act, (A.double() @ Bt.double().T + bias.double()).cpu().numpy())
     if resid:
         ref64 = ref64 + x0.double().cpu().numpy()
-    for v in ("10", "12"):
+    for v in ("10", "12", "12s2"):
         got = outs[v].double().cpu().numpy()
         err = np.abs(got - ref64) / np.maximum(np.abs(ref64), 1.0)
         assert err.max() < 8e-3, (v, err.max(), np.argwhere(err >= 8e-3)[:5].tolist())
     d = (outs["12"].float() - outs["10"].float()).abs() / outs["10"].float().abs().clamp(min=1.0)
     assert d.max().item() < 1.6e-2        # <= 2 bf16 ulps
+    assert torch.equal(outs["12"], outs["12s2"])     # the schedules differ in timing only
 
 
-@pytest.mark.parametrize("variant", ["10", "12"])
+@pytest.mark.parametrize("variant", ["10", "12", "12s2"])
 def test_gemm_statout_variants(L, cuda, monkeypatch, variant):
     """The producer-side LayerNorm partial statistics on both 256-tile kernels."""
-    monkeypatch.setenv("VTD_GEMM_VARIANT", variant)
+    monkeypatch.setenv("VTD_GEMM_VARIANT", variant[:2])
+    monkeypatch.setenv("VTD_W4_SCHED", "2" if variant.endswith("s2") else "1")
     M, N, K = 50176, 768, 768
     g = torch.Generator(device=cuda).manual_seed(5)
     A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)

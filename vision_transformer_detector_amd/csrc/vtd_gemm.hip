@@ -864,11 +864,14 @@ __global__ __launch_bounds__(BNT) void gemm_mx8_pp_kernel(
 bool gemm_w4_launch(int M, int N, int K, const bf16_t* A, int lda, const bf16_t* Bt, int ldb,
                     const vtd_epilogue* epi, int ngw, hipStream_t stream);
 
-// The bf16 256 x 256-tile kernel: 12 = w4 (vtd_gemm_w4.hip, one wave per SIMD, default),
-// 10 = pp2 (8-wave ping-pong).  Both compute the same products with the same epilogue
-// arithmetic; VTD_GEMM_VARIANT (read per call, for A/B in one process) picks one, any other
-// value means the default.
-constexpr int kDefaultVariant = 12;
+// The bf16 256 x 256-tile kernel: 10 = pp2 (8-wave ping-pong, default), 12 = w4
+// (vtd_gemm_w4.hip, one wave per SIMD, persistent).  Both compute the same products with the
+// same epilogue arithmetic; VTD_GEMM_VARIANT (read per call, for A/B in one process) picks
+// one, any other value means the default.  Measured (C2 B = 256 forward, two interleaved
+// rounds on one box, profiles/r03_fwd_ab.log): pp2 18.60k img/s, w4 17.89k (one barrier per
+// K-step) / 18.06k (two); isolated, w4 leads on qkv / mlp1 / head2 / 8192^3 and trails on
+// the residual layers (profiles/r03_gemm_w4_vs_pp2.jsonl).
+constexpr int kDefaultVariant = 10;
 int gemm_variant() {
   const char* v = getenv("VTD_GEMM_VARIANT");
   const int x = v ? atoi(v) : kDefaultVariant;

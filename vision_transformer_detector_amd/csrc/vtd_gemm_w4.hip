@@ -1,4 +1,4 @@
-// "w4": the bf16 Dense-layer GEMM with ONE wave per SIMD (vtd.py:297, 364-412, 454-493 as
+// "w4" (VTD_GEMM_VARIANT=12, opt-in): the bf16 Dense-layer GEMM with ONE wave per SIMD (vtd.py:297, 364-412, 454-493 as
 // C = act(A Bt^T + bias + rowadd) + resid; A [M][lda] and Bt [N][ldb] both K-contiguous).
 //
 // Tile 256 x 256, BK = 64, 256 threads = 4 waves in 2 (M) x 2 (N); each wave owns a
@@ -6,25 +6,23 @@
 // per lane (the register file is 512 per lane at one wave per SIMD: accumulators in AGPRs,
 // two fragment sets and the DMA offsets in VGPRs).  Against the 8-wave ping-pong pp2 tile
 // (128 x 64 per wave) every operand byte read from LDS feeds twice the MFMA work (128 KiB
-// of LDS reads per K-step instead of 192) and a K-step is 2 barriers instead of 8.
+// of LDS reads per K-step instead of 192) and a K-step is 1 barrier instead of 8.
 //
 // Staging: both operands HBM/L2 -> LDS by buffer_load_dwordx4 ... lds (1 KiB = 8 rows of
 // 128 B per wave-instruction, 16 per wave per K-step), two 64 KiB stages.  LDS rows are
 // 128 B with the 16-B chunk XOR-swizzled (A: chunk ^ (row & 7); B: the permuted-read
 // swizzle below), applied on the per-lane SOURCE address so the LDS image stays
 // lane-linear.  Fragments are double-buffered in registers (F0 = k 0..31 of a K-step,
-// F1 = k 32..63).  One K-step (kt, stage s = kt & 1):
+// F1 = k 32..63).  One K-step (kt, stage s = kt & 1), one barrier:
 //
-//   MFMA F0: 8, read F1(kt)          16 ds_read_b128
-//   MFMA F0: 8                       (F1's reads land meanwhile)
-//   lgkmcnt(0); barrier A            every wave has read all of stage s  (WAR)
-//   MFMA F0: 48, DMA tile kt+2 -> s  16 DMA instructions, 4 per 8 MFMAs
-//   vmcnt(16 | 0); barrier B         tile kt+1 (stage s^1) landed for every wave (RAW)
-//   MFMA F1: 64, read F0(kt+1)       2 reads per 8 MFMAs
+//   MFMA F0: 64, read F1(kt)             2 ds_read_b128 per 8 MFMAs (stage s)
+//   lgkmcnt(0); vmcnt(0); barrier        every wave has read all of stage s (WAR) and tile
+//                                        kt+1 (stage s^1, the only DMA in flight) landed (RAW)
+//   MFMA F1: 64, DMA tile kt+2 -> s,     2 DMA instructions + 2 ds_read_b128 per 8 MFMAs
+//     read F0(kt+1) (stage s^1)
 //
-// Tile kt + 2's DMA is issued right after barrier A of K-step kt and retired at barrier B
-// of K-step kt + 1: about 1.3 K-steps in flight.  Counted waits are inline asm and barriers raw s_barrier
-// (a __syncthreads() fence would drain the in-flight DMA).
+// Tile kt + 2's DMA thus has one K-step to land.  Counted waits are inline asm and the
+// barrier raw s_barrier (a __syncthreads() fence would drain the in-flight DMA).
 //
 // Epilogue: the MFMA operands are swapped (D = B-block x A-block^T) and the B fragment rows
 // permuted so that a lane holds 8 contiguous output columns of one output row: bias,
@@ -106,6 +104,16 @@ __device__ __forceinline__ void w4_dma(char* stage, const W4Src& s, int wave, in
                                            kt * 128, 0, 0);
 }
 
+__device__ __forceinline__ void w4_dma_a(char* stage, const W4Src& s, int wave, int kt, int j) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(s.ra, (w4_lds_t*)(stage + wave * 64 * 128 + j * 1024),
+                                           16, s.offa[j], kt * 128, 0, 0);
+}
+__device__ __forceinline__ void w4_dma_b(char* stage, const W4Src& s, int wave, int kt, int j) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(
+      s.rb, (w4_lds_t*)(stage + W4_OPND + wave * 64 * 128 + j * 1024), 16, s.offb[j], kt * 128, 0,
+      0);
+}
+
 __device__ __forceinline__ void w4_fence() {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("" ::: "memory");
@@ -141,55 +149,12 @@ __device__ __forceinline__ void w4_mfma_row(f32x4 (&acc)[8][8], const W4Frag& f,
     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.b[j], f.a[i], acc[i][j], 0, 0, 0);
 }
 
-// One K-step (see the file comment).  PF: tile kt + 2 exists (DMA it); NN: tile kt + 1
-// exists (read its first fragments).  Compile-time flags: no branch inside the step.
-template <bool PF, bool NN, int DG>
-__device__ __forceinline__ void w4_kstep0(f32x4 (&acc)[8][8], W4Frag& f0, W4Frag& f1, char* smem,
-                                         const W4Src& src, int kt, int wave, int aoff0,
-                                         int aoff1, int b00, int b01, int b10, int b11) {
-  char* st = smem + (kt & 1) * W4_STAGE;
-  char* nx = smem + ((kt + 1) & 1) * W4_STAGE;
-  w4_fence();
-  // ---- first quarter of F0's MFMAs, F1 reads (after the first row: the compiler's wait for
-  // F0's last reads of the previous step then does not also wait for these)
-  w4_mfma_row(acc, f0, 0);
-  w4_fence();
-#pragma unroll
-  for (int g = 0; g < 8; ++g) w4_read2(f1, st, g, aoff1, b10, b11);
-  w4_fence();
-  w4_mfma_row(acc, f0, 1);
-  w4_fence();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  w4_barrier();                                // A: stage st fully read by every wave
-  // ---- the rest of F0, DMA of tile kt + 2 into stage st (4 instructions per 8 MFMAs)
-#pragma unroll
-  for (int i = 2; i < 8; ++i) {
-    if (PF && !(DG & 1) && i < 6) {
-      w4_dma(st, src, wave, (DG & 2) ? 0 : kt + 2, 2 * (i - 2));
-      w4_dma(st, src, wave, (DG & 2) ? 0 : kt + 2, 2 * (i - 2) + 1);
-    }
-    w4_mfma_row(acc, f0, i);
-    w4_fence();
-  }
-  w4_fence();
-  if (PF) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  w4_barrier();                                // B: tile kt + 1 landed for every wave
-  // ---- F1's MFMAs, F0 reads of tile kt + 1 (B fragments first: the next K-step's first
-  // MFMA row needs all 8 of them)
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    if (NN) w4_read2(f0, nx, i, aoff0, b00, b01);
-    w4_mfma_row(acc, f1, i);
-    w4_fence();
-  }
-}
-
-// Schedule 1: one barrier per K-step.  F1(kt) is read during F0(kt)'s MFMAs; the barrier
+// One K-step kt (stage st = kt & 1 holds tile kt, F0(kt) in f0; see the file comment).
+// F1(kt) is read during F0(kt)'s MFMAs; the barrier
 // then retires both every wave's reads of stage st (WAR for tile kt + 2's DMA, issued during
 // F1's MFMAs) and tile kt + 1's DMA (RAW for F0(kt + 1)'s reads, also during F1's MFMAs).
 template <bool PF, bool NN, int DG>
-__device__ __forceinline__ void w4_kstep1(f32x4 (&acc)[8][8], W4Frag& f0, W4Frag& f1, char* smem,
+__device__ __forceinline__ void w4_kstep(f32x4 (&acc)[8][8], W4Frag& f0, W4Frag& f1, char* smem,
                                           const W4Src& src, int kt, int wave, int aoff0,
                                           int aoff1, int b00, int b01, int b10, int b11) {
   char* st = smem + (kt & 1) * W4_STAGE;
@@ -214,6 +179,65 @@ __device__ __forceinline__ void w4_kstep1(f32x4 (&acc)[8][8], W4Frag& f0, W4Frag
   }
 }
 
+// Two-barrier K-step (VTD_W4_SCHED=2): F1(kt) is read during the first quarter of F0's
+// MFMAs, so stage st is free a quarter of the way into the K-step and tile kt + 2's B
+// operand is DMA'd during F0's remaining MFMAs (its A operand during F1's):
+//   rows 0-3 of F0's MFMAs, read F1(kt) (4 per 8 MFMAs);  lgkmcnt(0); barrier A (stage st read
+//     by every wave)
+//   rows 4-7, DMA B(kt+2) (2 per 8 MFMAs);  vmcnt(8 | 0); barrier B (tile kt+1 landed: the 8
+//     youngest are kt+2's)
+//   F1's MFMAs, DMA A(kt+2) (1 per 8 MFMAs), read F0(kt+1) (stage st^1)
+// (Issuing DMA while F1's reads are in flight made the compiler spill: not done.)
+template <bool PF, bool NN, int DG>
+__device__ __forceinline__ void w4_kstep2(f32x4 (&acc)[8][8], W4Frag& f0, W4Frag& f1, char* smem,
+                                          const W4Src& src, int kt, int wave, int aoff0,
+                                          int aoff1, int b00, int b01, int b10, int b11) {
+  char* st = smem + (kt & 1) * W4_STAGE;
+  char* nx = smem + ((kt + 1) & 1) * W4_STAGE;
+  constexpr bool DMA = PF && !(DG & 1);
+  const int kd = (DG & 2) ? 0 : kt + 2;
+  w4_fence();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    w4_read2(f1, st, 2 * i, aoff1, b10, b11);
+    w4_read2(f1, st, 2 * i + 1, aoff1, b10, b11);
+    w4_mfma_row(acc, f0, i);
+    w4_fence();
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  w4_barrier();                                         // A
+#pragma unroll
+  for (int i = 4; i < 8; ++i) {
+    if (DMA) {
+      w4_dma_b(st, src, wave, kd, 2 * (i - 4));
+      w4_dma_b(st, src, wave, kd, 2 * (i - 4) + 1);
+    }
+    w4_mfma_row(acc, f0, i);
+    w4_fence();
+  }
+  if (DMA) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  w4_barrier();                                         // B
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (DMA) w4_dma_a(st, src, wave, kd, i);
+    if (NN) w4_read2(f0, nx, i, aoff0, b00, b01);
+    w4_mfma_row(acc, f1, i);
+    w4_fence();
+  }
+}
+
+// DMA of a tile's K-tiles 0 and 1 into stages 0 and 1 (the stages must be free: no wave
+// reads them any more)
+__device__ __forceinline__ void w4_issue_k01(char* smem, const W4Src& src, int wave, int nk) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) w4_dma(smem, src, wave, 0, j);
+  if (nk > 1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w4_dma(smem + W4_STAGE, src, wave, 1, j);
+  }
+}
+
 template <int SCHED, int DG>
 __device__ __forceinline__ void w4_mainloop(f32x4 (&acc)[8][8], char* smem, const W4Src& src,
                                             int nk, int wave, int wm, int wn, int lane) {
@@ -224,26 +248,22 @@ __device__ __forceinline__ void w4_mainloop(f32x4 (&acc)[8][8], char* smem, cons
   const int b00 = w4_swz_b(brow0, fg), b01 = w4_swz_b(brow1, fg);          // K-half 0
   const int b10 = w4_swz_b(brow0, 4 + fg), b11 = w4_swz_b(brow1, 4 + fg);  // K-half 1
 
-  // prologue: tiles 0 and 1 in flight, tile 0 landed
-#pragma unroll
-  for (int j = 0; j < 8; ++j) w4_dma(smem, src, wave, 0, j);
-  if (nk > 1) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) w4_dma(smem + W4_STAGE, src, wave, 1, j);
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
+  // K-tiles 0 and 1 were issued by w4_issue_k01 (for this tile, possibly during the previous
+  // tile's epilogue): at least 16 vector-memory operations are younger than K-tile 0's last
+  // DMA (K-tile 1's, or the previous epilogue's stores and this tile's column loads), so
+  // vmcnt(16) retires K-tile 0; with one K-tile only, everything is waited for
+  if (nk > 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   w4_barrier();
   W4Frag f0, f1;
 #pragma unroll
   for (int g = 0; g < 8; ++g) w4_read2(f0, smem, g, aoff0, b00, b01);
   int kt = 0;
-#define VTD_W4_STEP(PF, NN)                                                                    \
-  if constexpr (SCHED == 0)                                                                    \
-    w4_kstep0<PF, NN, DG>(acc, f0, f1, smem, src, kt, wave, aoff0, aoff1, b00, b01, b10, b11); \
-  else                                                                                         \
-    w4_kstep1<PF, NN, DG>(acc, f0, f1, smem, src, kt, wave, aoff0, aoff1, b00, b01, b10, b11);
+#define VTD_W4_STEP(PF, NN)                                                                   \
+  if constexpr (SCHED == 2)                                                                   \
+    w4_kstep2<PF, NN, DG>(acc, f0, f1, smem, src, kt, wave, aoff0, aoff1, b00, b01, b10, b11); \
+  else                                                                                        \
+    w4_kstep<PF, NN, DG>(acc, f0, f1, smem, src, kt, wave, aoff0, aoff1, b00, b01, b10, b11);
   for (; kt + 2 < nk; ++kt) {
     VTD_W4_STEP(true, true)
   }
@@ -268,42 +288,117 @@ __device__ __forceinline__ f32x4 w4_acc(const f32x4& a) {
 
 // Lane (fr, fg) of wave (wm, wn) holds output row m_base + 16 i + fr, columns
 // n_base + 32 jp + 8 fg + 0..7 = acc[i][2 jp] (first 4), acc[i][2 jp + 1] (last 4).
+// bias / colsum of a lane's 32 columns (4 x 8), loaded before the K loop (oldest memory
+// ops: the prologue's counted wait retires them, no load latency left in the epilogue)
+// EPI bit 16 (w4 only): the LayerNorm fold (epilogue.lnstat / colsum) is on
+constexpr int W4_LNFOLD = 16;
 template <int EPI>
+struct W4Cols {
+  static constexpr int NC = (EPI & W4_LNFOLD) ? 4 : 1;
+  f32x4 bias[4][2], cs[NC][2];
+};
+template <int EPI>
+__device__ __forceinline__ void w4_load_cols(W4Cols<EPI>& c, const EpiArgs& e, int n_base,
+                                             int lane) {
+  const int fg = lane >> 4;
+#pragma unroll
+  for (int jp = 0; jp < 4; ++jp)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int n = n_base + 32 * jp + 8 * fg + 4 * h;
+      c.bias[jp][h] = *reinterpret_cast<const f32x4*>(e.bias + n);
+      if constexpr ((EPI & W4_LNFOLD) != 0)
+        c.cs[jp][h] = *reinterpret_cast<const f32x4*>(e.colsum + n);
+    }
+}
+
+// residual rows of a lane: row block i, column pair jp, 16-B word w
+// (f32 residual: loaded two row blocks ahead of their use inside the epilogue)
+template <int EPI>
+struct W4Resid {
+  static constexpr int RW = (EPI & 4) ? 1 : 2;     // 16-B residual loads per 8 columns
+  i32x4 r[8][4][RW];
+};
+template <int EPI>
+__device__ __forceinline__ void w4_load_resid(W4Resid<EPI>& rr, const EpiArgs& e, int lane,
+                                              int m_base, int n_base, int i) {
+  const int fr = lane & 15, fg = lane >> 4;
+  const int64_t base = (int64_t)(m_base + 16 * i + fr) * e.ldr + n_base + 8 * fg;
+#pragma unroll
+  for (int jp = 0; jp < 4; ++jp)
+#pragma unroll
+    for (int w = 0; w < W4Resid<EPI>::RW; ++w) {
+      if constexpr ((EPI & 4) != 0)
+        rr.r[i][jp][w] =
+            *reinterpret_cast<const i32x4*>(static_cast<const bf16_t*>(e.resid) + base + 32 * jp);
+      else
+        rr.r[i][jp][w] = *reinterpret_cast<const i32x4*>(static_cast<const float*>(e.resid) +
+                                                         base + 32 * jp + 4 * w);
+    }
+}
+template <int EPI>
+constexpr bool w4_resid_preloaded() {
+  return (EPI & 8) != 0 && (EPI & 4) != 0;         // residual, bf16 stream
+}
+// bf16 residual: row blocks 0 .. W4_RPRE - 1 are loaded before the next tile's K-tile DMA is
+// issued (their waits never include that DMA); the epilogue loads the others two row blocks
+// ahead of their use (by then the DMA has had that long to land)
+constexpr int W4_RPRE = 3;
+
+// issue_next(): the next tile's K-tile DMA, issued as early as the epilogue allows: before
+// row block 0 without a residual, else right after the last residual load (a residual
+// load's wait must not include that DMA: vmcnt counts in issue order)
+template <int EPI, class F>
 __device__ __forceinline__ void w4_epilogue_direct(const f32x4 (&acc)[8][8], int lane, int m_base,
                                                    int n_base, const EpiArgs& e,
-                                                   const float2* lst) {
+                                                   const float2* lst, const W4Cols<EPI>& cols,
+                                                   W4Resid<EPI>& rres, F&& issue_next) {
   constexpr int ACT = EPI & 3;
+  constexpr bool LNF = (EPI & W4_LNFOLD) != 0;
   constexpr bool OUT_BF16 = (EPI & 4) != 0;
   constexpr bool RESID = (EPI & 8) != 0;
+  constexpr int RW = W4Resid<EPI>::RW;
   const int fr = lane & 15, fg = lane >> 4;
+  // residual rows two row blocks ahead of their use (one wave per SIMD: nothing else hides
+  // a load's latency); bf16: the first W4_RPRE preloaded by the caller
+  auto& rr = rres.r;
+  auto load_rows = [&](int i) { w4_load_resid<EPI>(rres, e, lane, m_base, n_base, i); };
+  constexpr int PRE = w4_resid_preloaded<EPI>() ? W4_RPRE : 0;   // row blocks already loaded
+  if constexpr (RESID) {
+#pragma unroll
+    for (int i = PRE; i < 2; ++i) load_rows(i);
+  } else {
+    issue_next();
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
+    if constexpr (RESID) {
+      if (i + 2 < 8 && i + 2 >= PRE) load_rows(i + 2);
+      if (i + 2 == 7 || (i == 0 && PRE >= 8)) issue_next();
+    }
     w4_fence();                    // one row block at a time: no hoisted accumulator copies
     const int lr = 16 * i + fr, mrow = m_base + lr;
-    f32x4 rv[4][2];
-    if constexpr (RESID) {
-#pragma unroll
-      for (int jp = 0; jp < 4; ++jp)
-        load_resid8<OUT_BF16>(e, (int64_t)mrow * e.ldr + n_base + 32 * jp + 8 * fg, rv[jp][0],
-                              rv[jp][1]);
-    }
     float tsum[2] = {0.f, 0.f};
     i32x4 ob[4];
 #pragma unroll
     for (int jp = 0; jp < 4; ++jp) {
       f32x4 v0 = w4_acc(acc[i][2 * jp]), v1 = w4_acc(acc[i][2 * jp + 1]);
       const int ncol = n_base + 32 * jp + 8 * fg;
-      // bias / colsum re-read per row block (L1 hits): keeps 64 registers free
-      if (e.lnstat)
-        epi_lnfold8(e, lst, mrow, lr, *reinterpret_cast<const f32x4*>(e.colsum + ncol),
-                    *reinterpret_cast<const f32x4*>(e.colsum + ncol + 4), v0, v1);
-      v0 += *reinterpret_cast<const f32x4*>(e.bias + ncol);
-      v1 += *reinterpret_cast<const f32x4*>(e.bias + ncol + 4);
+      if constexpr (LNF)
+        epi_lnfold8(e, lst, mrow, lr, cols.cs[jp][0], cols.cs[jp][1], v0, v1);
+      v0 += cols.bias[jp][0];
+      v1 += cols.bias[jp][1];
       if (e.rowadd) epi_rowadd8(e, mrow, ncol, v0, v1);
       act_ct8<ACT>(v0, v1);
       if constexpr (RESID) {
-        v0 += rv[jp][0];
-        v1 += rv[jp][1];
+        if constexpr (OUT_BF16) {
+          const i32x4 w = rr[i][jp][0];
+          v0 += bf16x4_to_f32((uint32_t)w[0], (uint32_t)w[1]);
+          v1 += bf16x4_to_f32((uint32_t)w[2], (uint32_t)w[3]);
+        } else {
+          v0 += __builtin_bit_cast(f32x4, rr[i][jp][0]);
+          v1 += __builtin_bit_cast(f32x4, rr[i][jp][RW - 1]);
+        }
       }
       if (e.out2) epi_out2_8(e, mrow, ncol, v0, v1);
       const int64_t idx = (int64_t)mrow * e.ldo + ncol;
@@ -358,6 +453,23 @@ __device__ __forceinline__ void w4_epilogue_generic(const f32x4 (&acc)[8][8], fl
   }
 }
 
+// tile vb's (m0, n0): XCD-aware bijective remap (blocks b, b + 8, ... share an XCD: each
+// XCD walks one contiguous chunk of the tile order) + n-group tile order
+__device__ __forceinline__ void w4_tile(int vb, int tiles_m, int tiles_n, int ngw, int& m0,
+                                        int& n0) {
+  const int nwg = tiles_m * tiles_n;
+  const int xcd = vb & 7, q = nwg >> 3, r = nwg & 7;
+  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (vb >> 3);
+  int tm, tn;
+  tile_coords(tile, tiles_m, tiles_n, ngw, tm, tn);
+  m0 = tm * W4_TILE;
+  n0 = tn * W4_TILE;
+}
+
+// Persistent: a grid of min(tiles, CUs) workgroups; workgroup b takes tiles vb = b, b + G,
+// ... (G a multiple of 8 keeps each XCD on its chunk).  The next tile's K-tiles 0 and 1 are
+// DMA'd into the stages while the current tile's epilogue runs (it reads no LDS), so a
+// tile's prologue load latency is hidden behind the previous tile's epilogue.
 template <int EPI, int SCHED = 1, int DG = 0>
 __global__ __launch_bounds__(W4_T, 1) void gemm_tn_bf16_w4_kernel(
     int M, int N, int K, const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ Bt,
@@ -366,56 +478,92 @@ __global__ __launch_bounds__(W4_T, 1) void gemm_tn_bf16_w4_kernel(
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  // XCD-aware bijective remap (blocks b, b + 8, ... share an XCD) + n-group tile order
-  const int nwg = tiles_m * tiles_n, bid = blockIdx.x;
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  int tm, tn;
-  tile_coords(tile, tiles_m, tiles_n, e.ngw, tm, tn);
-  const int m0 = tm * W4_TILE, n0 = tn * W4_TILE;
+  const int T = tiles_m * tiles_n, G = gridDim.x, nk = K / 64;
+  int vb = blockIdx.x;
+  if (vb >= T) return;                         // uniform per workgroup
+  int m0, n0;
+  w4_tile(vb, tiles_m, tiles_n, e.ngw, m0, n0);
   W4Src src;
   w4_sources(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane);
-  // LayerNorm-fold row statistics of the wave's 128 rows (oldest vector-memory ops: the
-  // prologue's counted wait retires them); lane l holds rows l and 64 + l
-  float2 lst[2] = {float2{0.f, 0.f}, float2{0.f, 0.f}};
-  if (e.lnstat) {
-    lst[0] = e.lnstat[min(m0 + wm * 128 + lane, M - 1)];
-    lst[1] = e.lnstat[min(m0 + wm * 128 + 64 + lane, M - 1)];
-  }
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  w4_mainloop<SCHED, DG>(acc, smem, src, K / 64, wave, wm, wn, lane);
-  const int m_base = m0 + wm * 128, n_base = n0 + wn * 128;
-  if constexpr (EPI != EPI_GENERIC) {
-    if (m0 + W4_TILE <= M && n0 + W4_TILE <= N) {
-      w4_epilogue_direct<EPI>(acc, lane, m_base, n_base, e, lst);
-      return;
+  w4_issue_k01(smem, src, wave, nk);
+  for (;;) {
+    // LayerNorm-fold row statistics of the wave's 128 rows (lane l holds rows l, 64 + l) and
+    // the lane's bias / colsum columns: used in the epilogue only
+    float2 lst[2] = {float2{0.f, 0.f}, float2{0.f, 0.f}};
+    if ((EPI & W4_LNFOLD) != 0 || EPI == EPI_GENERIC) {
+      lst[0] = e.lnstat[min(m0 + wm * 128 + lane, M - 1)];
+      lst[1] = e.lnstat[min(m0 + wm * 128 + 64 + lane, M - 1)];
     }
+    const int m_base = m0 + wm * 128, n_base = n0 + wn * 128;
+    const bool full = m0 + W4_TILE <= M && n0 + W4_TILE <= N;
+    W4Cols<EPI> cols;
+    if constexpr (EPI != EPI_GENERIC) {
+      if (full) w4_load_cols(cols, e, n_base, lane);
+    }
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    w4_mainloop<SCHED, DG>(acc, smem, src, nk, wave, wm, wn, lane);
+    // every wave passed the last K-step's barrier: no LDS read of this tile is pending
+    const int vn = vb + G;
+    const bool more = vn < T;
+    int m1 = 0, n1 = 0;
+    if (more) w4_tile(vn, tiles_m, tiles_n, e.ngw, m1, n1);
+    if constexpr (EPI != EPI_GENERIC) {
+      if (full) {
+        W4Resid<EPI> rr;
+        if constexpr (w4_resid_preloaded<EPI>()) {
+#pragma unroll
+          for (int i = 0; i < W4_RPRE; ++i) w4_load_resid<EPI>(rr, e, lane, m_base, n_base, i);
+        }
+        w4_epilogue_direct<EPI>(acc, lane, m_base, n_base, e, lst, cols, rr, [&] {
+          if (more) {
+            w4_sources(src, A, lda, M, Bt, ldb, N, m1, n1, wave, lane);
+            w4_issue_k01(smem, src, wave, nk);
+          }
+        });
+        if (!more) return;
+        vb = vn;
+        m0 = m1;
+        n0 = n1;
+        continue;
+      }
+    }
+    // staged epilogue: it uses the stages, so the next tile's DMA waits for every wave
+    w4_epilogue_generic(acc, reinterpret_cast<float*>(smem) + wave * 32 * W4_ES, lane, M, N,
+                        m_base, n_base, e);
+    if (!more) return;
+    w4_fence();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    w4_barrier();
+    vb = vn;
+    m0 = m1;
+    n0 = n1;
+    w4_sources(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane);
+    w4_issue_k01(smem, src, wave, nk);
   }
-  w4_epilogue_generic(acc, reinterpret_cast<float*>(smem) + wave * 32 * W4_ES, lane, M, N,
-                      m_base, n_base, e);
 }
 
-template <int C, int SCHED, int DG = 0>
+template <int C, int SCHED = 1, int DG = 0>
 void w4_launch(dim3 g, hipStream_t stream, int M, int N, int K, const bf16_t* A, int lda,
                const bf16_t* Bt, int ldb, int tiles_m, int tiles_n, const EpiArgs& e) {
   static std::once_flag once[kMaxDevices];
   once_per_device(once, [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_bf16_w4_kernel<C, SCHED, DG>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, W4_LDS);
+    (void)hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&gemm_tn_bf16_w4_kernel<C, SCHED, DG>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, W4_LDS);
   });
   hipLaunchKernelGGL((gemm_tn_bf16_w4_kernel<C, SCHED, DG>), g, dim3(W4_T), W4_LDS, stream, M, N,
                      K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
 }
 
-// K-loop schedule (VTD_W4_SCHED, read per call: A/B in one process; both exact):
-// 1 = one barrier per K-step (default), 0 = two barriers per K-step
+// K-step schedule (VTD_W4_SCHED, read per call: A/B in one process; both exact):
+// 1 = one barrier per K-step, 2 = two (earlier DMA of tile kt + 2)
 int w4_sched() {
   const char* v = getenv("VTD_W4_SCHED");
-  return v && atoi(v) == 0 ? 0 : 1;
+  return v && atoi(v) == 2 ? 2 : 1;
 }
 
 }  // namespace
@@ -430,36 +578,40 @@ bool gemm_w4_launch(int M, int N, int K, const bf16_t* A, int lda, const bf16_t*
   const bool fast = e.bias && !e.dets && e.scatter_tokens <= 0 && e.ldo % 8 == 0 &&
                     (!e.resid || e.ldr % 8 == 0) && a16(e.out) && a16(e.bias) &&
                     (!e.resid || a16(e.resid)) && (!e.out2 || (e.ldo2 % 8 == 0 && a16(e.out2)));
-  const int code = fast ? epi_code(e.act, e.out_dtype == VTD_BF16, e.resid != nullptr)
-                        : EPI_GENERIC;
+  // the LayerNorm fold is a compile-time epilogue property (bit 16): its column sums and a
+  // residual never share a kernel (no forward layer has both: those go the generic way)
+  const int code = fast && !(e.lnstat && e.resid)
+                       ? epi_code(e.act, e.out_dtype == VTD_BF16, e.resid != nullptr) |
+                             (e.lnstat ? W4_LNFOLD : 0)
+                       : EPI_GENERIC;
   const int tiles_m = (M + W4_TILE - 1) / W4_TILE, tiles_n = (N + W4_TILE - 1) / W4_TILE;
-  const dim3 g(tiles_m * tiles_n);
+  const dim3 g(std::min(tiles_m * tiles_n, device_cu_count()));
 #if VTD_DIAG
-  // timing diagnostics (wrong outputs), plain bf16 epilogue only: VTD_W4_DG = 1 / 2 / 3
+  // timing diagnostics (wrong outputs), plain bf16 epilogue only: VTD_W4_DG = 1 / 2
   if (const char* dg = getenv("VTD_W4_DG"); dg && atoi(dg) > 0 && code == 4) {
     const int d = atoi(dg);
     if (d == 1) w4_launch<4, 1, 1>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
     else if (d == 2) w4_launch<4, 1, 2>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
-    else w4_launch<4, 0, 1>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
+    else if (d == 3) w4_launch<4, 2, 1>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
+    else w4_launch<4, 2, 2>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
     return true;
   }
 #endif
   const int sched = w4_sched();
   switch (code) {
-#define VTD_W4_CASE(C)                                                                        \
-  case C:                                                                                     \
-    if (sched == 1) w4_launch<C, 1>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e); \
-    else w4_launch<C, 0>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);          \
+#define VTD_W4_CASE(C)                                                                       \
+  case C:                                                                                    \
+    if (sched == 2) w4_launch<C, 2>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e); \
+    else w4_launch<C, 1>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);          \
     break;
     VTD_W4_CASE(0) VTD_W4_CASE(1) VTD_W4_CASE(2) VTD_W4_CASE(4) VTD_W4_CASE(5) VTD_W4_CASE(6)
     VTD_W4_CASE(8) VTD_W4_CASE(9) VTD_W4_CASE(10) VTD_W4_CASE(12) VTD_W4_CASE(13)
-    VTD_W4_CASE(14)
+    VTD_W4_CASE(14) VTD_W4_CASE(16) VTD_W4_CASE(17) VTD_W4_CASE(18) VTD_W4_CASE(20)
+    VTD_W4_CASE(21) VTD_W4_CASE(22)
 #undef VTD_W4_CASE
     default:
-      if (sched == 1)
-        w4_launch<EPI_GENERIC, 1>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
-      else
-        w4_launch<EPI_GENERIC, 0>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
+      if (sched == 2) w4_launch<EPI_GENERIC, 2>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
+      else w4_launch<EPI_GENERIC, 1>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
   }
   return true;
 }
