@@ -286,3 +286,38 @@ def test_load_weights_from_keras_hdf5(vtd, cuda, dtype):
         assert np.array_equal(v, w[k]), k
     ok, rel = within(model(torch.from_numpy(x).to(cuda)).cpu().numpy(), expect, TOL[dtype])
     assert ok, f"{dtype}: max rel err {rel:.3e}"
+
+
+REMOVED_SWITCHES = {
+    # round-2 diagnostic / measured-negative kernels, removed in round 3
+    "VTD_GEMM_VARIANT": ["2", "3", "5", "21", "24", "27", "30", "33", "36"],
+    "VTD_ATTN_DIAG": ["1", "2"],
+    "VTD_PP3_DIAG": ["1"],
+    "VTD_LN_FUSE": ["1"],
+}
+
+
+def test_removed_diagnostic_switches_do_not_change_logits(vtd, cuda, monkeypatch):
+    """The switches that selected round-2 diagnostic or wrong-output kernels are gone: with
+    any of them set, the forward gives the default path's bits (C2 batch 8 bf16 takes the
+    pp2 GEMM tiles and the persistent attention kernel; tiny_gelu the small-tile paths)."""
+    spec = json.load(open(os.path.join(GOLD, "seeded_forward.json")))["c2_vitb16_b1"]
+    kw = dict(spec["kwargs"])
+    w = V.init_weights(seed=spec["weight_seed"], perturb=spec["perturb"], **kw)
+    shape = V.resolve_kwargs(**kw)["input_shape"]
+    x = torch.from_numpy(V.synthetic_images(8, shape, seed=3)).to(cuda)
+    tkw, tw, tx, _, _ = load_tiny("tiny_gelu")
+    tx = torch.from_numpy(tx).to(cuda)
+    for var in REMOVED_SWITCHES:
+        monkeypatch.delenv(var, raising=False)
+    big = vtd.create_vision_transformer_detector(**kw, dtype="bfloat16")
+    big.set_weights(w)
+    tiny = vtd.create_vision_transformer_detector(**tkw, dtype="bfloat16")
+    tiny.set_weights(tw)
+    ref_big, ref_tiny = big(x), tiny(tx)
+    for var, values in REMOVED_SWITCHES.items():
+        for val in values:
+            monkeypatch.setenv(var, val)
+            assert torch.equal(big(x), ref_big), (var, val)
+            assert torch.equal(tiny(tx), ref_tiny), (var, val)
+        monkeypatch.delenv(var)

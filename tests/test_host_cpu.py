@@ -39,6 +39,16 @@ def test_library_exports_every_declared_symbol(L):
     assert L.lib.vtd_abi_version() == L.ABI_VERSION
 
 
+def test_removed_switches_are_not_read_by_the_library(L):
+    """The round-2 diagnostic switches (VTD_ATTN_DIAG, VTD_PP3_DIAG, VTD_LN_FUSE) are gone
+    from the product library: their names are not in libvtd.so's strings, so no getenv can
+    read them (the GPU test checks the logits with them set)."""
+    blob = open(L.lib._name, "rb").read()
+    for name in (b"VTD_ATTN_DIAG", b"VTD_PP3_DIAG", b"VTD_LN_FUSE", b"VTD_W4_DG"):
+        assert name + b"\0" not in blob, name
+    assert b"VTD_GEMM_VARIANT\0" in blob   # the live A/B switch: 10 (default) or 12
+
+
 def test_ctypes_struct_layout_matches_c(L):
     """Compile a probe against include/vtd.h with gcc and compare sizeof/offsetof."""
     src = r'''
