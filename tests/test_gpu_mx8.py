@@ -2,7 +2,8 @@
   - vtd_quantize_mx8 against the CPU restatement oracle/mx8.py, element for element
     (e4m3 values and E8M0 block exponents must be identical);
   - vtd_gemm_mx8 against the fp64 product of the DEQUANTIZED device operands, so the
-    check isolates the block-scaled MFMA + fp32 accumulation + epilogue.  Tolerance
+    check isolates the block-scaled MFMA + fp32 accumulation + epilogue; both MX kernels
+    (VTD_MX_VARIANT 1 = 8-wave ping-pong, 2 = x4, one wave per SIMD).  Tolerance
     5e-4 relative for f32 outputs: the instruction reduces each 128-element K-step
     inside the matrix core before the fp32 accumulate (measured max 1.1e-4 at K <= 1536,
     6x the 2e-5 of the bf16 MFMA's exact fp32 fma chain); 8e-3 for bf16 outputs.
@@ -65,8 +66,12 @@ def test_quantize_matches_oracle(L, cuda, rows, K, Kq, src):
 @pytest.mark.parametrize("M,N,K,act,out_dtype,resid", [
     (300, 200, 256, 0, 0, False), (1000, 520, 384, 1, 1, False),
     (4096, 1024, 1024, 1, 1, False), (2600, 776, 1536, 0, 0, True),
-    (513, 64, 128, 2, 0, False), (4096, 768, 1536, 1, 1, True), (1000, 520, 384, 0, 1, True)])
-def test_gemm_mx8_matches_dequantized_fp64(L, cuda, M, N, K, act, out_dtype, resid):
+    (513, 64, 128, 2, 0, False), (4096, 768, 1536, 1, 1, True), (1000, 520, 384, 0, 1, True),
+    (2304, 1280, 640, 2, 1, False)])
+@pytest.mark.parametrize("variant", ["1", "2"])
+def test_gemm_mx8_matches_dequantized_fp64(L, cuda, monkeypatch, variant, M, N, K, act,
+                                           out_dtype, resid):
+    monkeypatch.setenv("VTD_MX_VARIANT", variant)
     g = torch.Generator(device=cuda).manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
     W = torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)
@@ -98,10 +103,13 @@ def test_gemm_mx8_matches_dequantized_fp64(L, cuda, M, N, K, act, out_dtype, res
     assert err.max() < tol, (err.max(), np.argwhere(err >= tol)[:5].tolist())
 
 
-@pytest.mark.parametrize("rows,D,x_dtype", [(200, 768, "bf16"), (64, 1024, "f32"), (37, 96, "bf16")])
+@pytest.mark.parametrize("rows,D,x_dtype", [(200, 768, "bf16"), (64, 1024, "f32"), (37, 96, "bf16"),
+                                             (50, 104, "bf16"), (21, 2048, "bf16"),
+                                             (9, 4000, "f32")])
 def test_layernorm_mx8_equals_layernorm_then_quantize(L, cuda, rows, D, x_dtype):
     """The fused LayerNorm -> MX-fp8 pass writes exactly the bytes of vtd_layernorm (bf16 out)
-    followed by vtd_quantize_mx8."""
+    followed by vtd_quantize_mx8: the 16-columns-per-lane pair (D % 16 == 0) and the 4-column
+    pair (D = 104)."""
     g = torch.Generator(device=cuda).manual_seed(rows + D)
     xdt = torch.bfloat16 if x_dtype == "bf16" else torch.float32
     x = (torch.randn(rows, D, generator=g, device=cuda) * 3 + 1).to(xdt)
@@ -124,10 +132,14 @@ def test_layernorm_mx8_equals_layernorm_then_quantize(L, cuda, rows, D, x_dtype)
     assert torch.equal(s.view(Kq // 128, s_rows, 4)[:, :rows], s_ref_v)
 
 
-@pytest.mark.parametrize("M,N,K,act", [(4096, 1024, 1024, 1), (2560, 512, 384, 0)])
-def test_gemm_mx8_fp8_output_equals_quantized_bf16_output(L, cuda, M, N, K, act):
+@pytest.mark.parametrize("M,N,K,act", [(4096, 1024, 1024, 1), (2560, 512, 384, 0),
+                                       (1536, 2048, 768, 2)])
+@pytest.mark.parametrize("variant", ["1", "2"])
+def test_gemm_mx8_fp8_output_equals_quantized_bf16_output(L, cuda, monkeypatch, variant, M, N,
+                                                          K, act):
     """out_dtype VTD_FP8 (the next MX GEMM's operand written by the epilogue) equals the bf16
     output of the same GEMM passed through vtd_quantize_mx8, byte for byte."""
+    monkeypatch.setenv("VTD_MX_VARIANT", variant)
     g = torch.Generator(device=cuda).manual_seed(M + N + K + 7)
     A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
     W = torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)
@@ -154,6 +166,35 @@ def test_gemm_mx8_fp8_output_equals_quantized_bf16_output(L, cuda, M, N, K, act)
     torch.cuda.synchronize()
     assert torch.equal(q, q_ref)
     assert torch.equal(s, s_ref)
+
+
+@pytest.mark.parametrize("M,N,K,act,resid", [(4096, 1024, 1024, 0, False),
+                                              (2048, 768, 1536, 1, True),
+                                              (777, 300, 384, 2, False)])
+def test_gemm_mx8_x4_equals_pingpong(L, cuda, monkeypatch, M, N, K, act, resid):
+    """The two MX kernels compute each output as the same sequence of 128-wide scaled MFMA
+    K-steps accumulated in fp32 in K order (x4 with the operands swapped: D^T = B A^T), so
+    their outputs agree bit for bit."""
+    g = torch.Generator(device=cuda).manual_seed(M * 3 + N + K)
+    A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
+    W = torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)
+    qa, sa, sa_rows = _quantize(L, A, K)
+    qb, sb, sb_rows = _quantize(L, W, K)
+    bias = torch.randn(N, generator=g, device=cuda)
+    res = torch.randn(M, N, generator=g, device=cuda).to(torch.bfloat16) if resid else None
+    outs = []
+    for variant in ("1", "2"):
+        monkeypatch.setenv("VTD_MX_VARIANT", variant)
+        out = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
+        e = L.VtdEpilogue()
+        e.bias, e.act, e.out, e.ldo, e.out_dtype = bias.data_ptr(), act, out.data_ptr(), N, 1
+        e.resid, e.ldr = (res.data_ptr(), N) if resid else (None, 0)
+        L.check(L.lib.vtd_gemm_mx8(M, N, K, qa.data_ptr(), K, sa.data_ptr(), sa_rows,
+                                   qb.data_ptr(), K, sb.data_ptr(), sb_rows, ctypes.byref(e),
+                                   L.stream_ptr()), "gemm_mx8")
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]), (outs[0].float() - outs[1].float()).abs().max().item()
 
 
 @pytest.mark.parametrize("B,N,H,dkp", [(2, 196, 12, 64), (1, 576, 16, 64), (3, 100, 4, 32),

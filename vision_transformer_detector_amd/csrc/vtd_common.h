@@ -117,6 +117,26 @@ __device__ __forceinline__ float decode_transform(int f, float v) {
 
 // bf16 rounding of an f32 value, back in f32 (the fused quantizers quantize what the
 // unfused path would have stored as bf16)
+// Sum over the 64 lanes in the butterfly order s += s[l ^ o], o = 32, 16, 8, 4, 2, 1 (every
+// lane ends with the total; the same bits as that __shfl_xor loop: each step adds the same
+// two values) without the LDS round trips of ds_bpermute: the gfx950 lane swaps for 32 / 16,
+// DPP for the rest.  After the xor-8 step lanes l and l ^ 8 agree, so row_ror:4 (lane
+// (l + 4) mod 16) delivers the value of l ^ 4.
+template <int CTRL>
+__device__ __forceinline__ float dpp_get(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum(float s) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  s = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  r = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  s = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  s += dpp_get<0x128>(s);   // row_ror:8  (l ^ 8 within the 16-lane row)
+  s += dpp_get<0x124>(s);   // row_ror:4  (l ^ 4, see above)
+  s += dpp_get<0x4E>(s);    // quad_perm [2, 3, 0, 1]
+  s += dpp_get<0xB1>(s);    // quad_perm [1, 0, 3, 2]
+  return s;
+}
 __device__ __forceinline__ float bf16_round(float v) {
   return __uint_as_float((uint32_t)f32_to_bf16(v) << 16);
 }

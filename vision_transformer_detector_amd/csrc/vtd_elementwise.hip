@@ -40,8 +40,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(
     v[i] = c < D ? ld4(xr + c) : f32x4{0.f, 0.f, 0.f, 0.f};
     s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  s = wave_sum(s);
   const float mean = s / D;
   float q = 0.f;
 #pragma unroll
@@ -54,8 +53,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(
         q += d * d;
       }
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+  q = wave_sum(q);
   const float rstd = 1.f / sqrtf(q / D + eps);
   TO* yr = y + row * ldy;
 #pragma unroll
@@ -85,18 +83,180 @@ __global__ __launch_bounds__(256) void layernorm_generic_kernel(
   const TI* xr = x + row * ldx;
   float s = 0.f;
   for (int c = lane; c < D; c += 64) s += DT<TI>::load(xr + c);
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  s = wave_sum(s);
   const float mean = s / D;
   float q = 0.f;
   for (int c = lane; c < D; c += 64) {
     const float d = DT<TI>::load(xr + c) - mean;
     q += d * d;
   }
-  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+  q = wave_sum(q);
   const float rstd = 1.f / sqrtf(q / D + eps);
   TO* yr = y + row * ldy;
   for (int c = lane; c < ldy; c += 64)
     yr[c] = DT<TO>::from(c < D ? (DT<TI>::load(xr + c) - mean) * rstd * gamma[c] + beta[c] : 0.f);
+}
+
+// ---- 16 columns per lane (D % 16 == 0): the wide LayerNorm pair.  layernorm16_kernel and
+// layernorm16_mx8_kernel share the load and the statistics below (same lane layout, same
+// reduction order: the MX-fp8 bytes equal layernorm16's bf16 output quantized), and move
+// 16-B vectors per lane: 32 B of bf16 in, 16 B of e4m3 out (a 32-column MX block is a lane
+// pair: one DPP step for its amax).  Lane l of chunk i owns columns 16 (64 i + l) .. + 15.
+template <int NC>
+struct Ln16Row {
+  f32x4 v[NC][4];
+};
+__device__ __forceinline__ void ld16(const bf16_t* p, f32x4 (&v)[4]) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint4 w = *reinterpret_cast<const uint4*>(p + 8 * h);
+    v[2 * h] = f32x4{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+                     __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)};
+    v[2 * h + 1] = f32x4{__uint_as_float(w.z << 16), __uint_as_float(w.z & 0xffff0000u),
+                         __uint_as_float(w.w << 16), __uint_as_float(w.w & 0xffff0000u)};
+  }
+}
+__device__ __forceinline__ void ld16(const float* p, f32x4 (&v)[4]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) v[g] = *reinterpret_cast<const f32x4*>(p + 4 * g);
+}
+template <typename TI, int NC>
+__device__ __forceinline__ void ln16_load(Ln16Row<NC>& r, const TI* xr, int D, int lane) {
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const int c = (i * 64 + lane) * 16;
+    if (c < D) {
+      ld16(xr + c, r.v[i]);
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) r.v[i][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+}
+template <int NC>
+__device__ __forceinline__ void ln16_stats(const Ln16Row<NC>& r, int D, int lane, float eps,
+                                           float& mean, float& rstd) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NC; ++i)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) s += r.v[i][g][0] + r.v[i][g][1] + r.v[i][g][2] + r.v[i][g][3];
+  mean = wave_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    if ((i * 64 + lane) * 16 < D)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float d = r.v[i][g][j] - mean;
+          q += d * d;
+        }
+  }
+  rstd = 1.f / sqrtf(wave_sum(q) / D + eps);
+}
+// the normalized, affine-transformed 16 values of chunk i (bf16-rounded for the MX path)
+template <int NC, bool ROUND>
+__device__ __forceinline__ void ln16_out(const Ln16Row<NC>& r, int i, int c, float mean,
+                                         float rstd, const float* gamma, const float* beta,
+                                         f32x4 (&o)[4]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const f32x4 ga = *reinterpret_cast<const f32x4*>(gamma + c + 4 * g);
+    const f32x4 be = *reinterpret_cast<const f32x4*>(beta + c + 4 * g);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float v = (r.v[i][g][j] - mean) * rstd * ga[j] + be[j];
+      o[g][j] = ROUND ? bf16_round(v) : v;
+    }
+  }
+}
+
+template <typename TI, typename TO, int NC, int RPW>
+__global__ __launch_bounds__(256) void layernorm16_kernel(
+    const TI* __restrict__ x, int64_t rows, int D, int ldx, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, TO* __restrict__ y, int ldy) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (row0 >= rows) return;
+  Ln16Row<NC> r[RPW];
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) ln16_load(r[k], x + min(row0 + k, rows - 1) * ldx, D, lane);
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) {
+    const int64_t row = row0 + k;
+    if (row >= rows) break;
+    float mean, rstd;
+    ln16_stats(r[k], D, lane, eps, mean, rstd);
+    TO* yr = y + row * ldy;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int c = (i * 64 + lane) * 16;
+      if (c < D) {
+        f32x4 o[4];
+        ln16_out<NC, false>(r[k], i, c, mean, rstd, gamma, beta, o);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) st4(yr + c + 4 * g, o[g]);
+      }
+    }
+    for (int c = D + lane; c < ldy; c += 64) yr[c] = DT<TO>::from(0.f);
+  }
+}
+
+template <typename TI, int NC, int RPW>
+__global__ __launch_bounds__(256) void layernorm16_mx8_kernel(
+    const TI* __restrict__ x, int64_t rows, int D, int ldx, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, uint8_t* __restrict__ q, int ldq, int Kq,
+    uint8_t* __restrict__ sc, int64_t s_rows) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (row0 >= rows) return;
+  Ln16Row<NC> r[RPW];
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) ln16_load(r[k], x + min(row0 + k, rows - 1) * ldx, D, lane);
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) {
+    const int64_t row = row0 + k;
+    if (row >= rows) break;
+    float mean, rstd;
+    ln16_stats(r[k], D, lane, eps, mean, rstd);
+    uint8_t* qr = q + row * ldq;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const int c = (i * 64 + lane) * 16;
+      f32x4 o[4] = {};
+      if (c < D) ln16_out<NC, true>(r[k], i, c, mean, rstd, gamma, beta, o);
+      float am = 0.f;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        am = fmaxf(am, fmaxf(fmaxf(fabsf(o[g][0]), fabsf(o[g][1])),
+                             fmaxf(fabsf(o[g][2]), fabsf(o[g][3]))));
+      am = fmaxf(am, dpp_get<0xB1>(am));               // the lane pair of the 32-block
+      const int E = mx8_exponent(am);
+      const float inv = __uint_as_float((uint32_t)(127 - E) << 23);
+      if (c < Kq) {
+        uint4 w;
+        w.x = mx8_pack4(o[0][0], o[0][1], o[0][2], o[0][3], inv);
+        w.y = mx8_pack4(o[1][0], o[1][1], o[1][2], o[1][3], inv);
+        w.z = mx8_pack4(o[2][0], o[2][1], o[2][2], o[2][3], inv);
+        w.w = mx8_pack4(o[3][0], o[3][1], o[3][2], o[3][3], inv);
+        *reinterpret_cast<uint4*>(qr + c) = w;
+        if ((lane & 1) == 0) {
+          const int b = c >> 5;
+          sc[((int64_t)(b >> 2) * s_rows + row) * 4 + (b & 3)] = (uint8_t)(E + 127);
+        }
+      }
+    }
+  }
+}
+
+// whether the 16-column LayerNorms apply (the plain and the MX-fp8 one decide alike, so the
+// two give the same statistics for the same input)
+bool ln16_ok(const void* x, int x_dtype, int D, int ldx, const float* g, const float* b) {
+  auto al16 = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
+  return D % 16 == 0 && D <= 4096 && ldx % (x_dtype == VTD_BF16 ? 8 : 4) == 0 && al16(x) &&
+         al16(g) && al16(b);
 }
 
 template <typename TI, typename TO>
@@ -110,6 +270,19 @@ int ln_dispatch(const void* xv, int64_t rows, int D, int ldx, const float* g,
                    (reinterpret_cast<uintptr_t>(y) % (4 * sizeof(TO)) == 0) &&
                    (reinterpret_cast<uintptr_t>(g) % 16 == 0) &&
                    (reinterpret_cast<uintptr_t>(b) % 16 == 0);
+  if (vec && ln16_ok(xv, sizeof(TI) == 2 ? VTD_BF16 : VTD_F32, D, ldx, g, b)) {
+    constexpr int RPW = 2;
+    const dim3 g16((unsigned)((rows + 4 * RPW - 1) / (4 * RPW)));
+    const int nc = (D + 1023) / 1024;
+#define VTD_LN16(NC) hipLaunchKernelGGL((layernorm16_kernel<TI, TO, NC, RPW>), g16, block, 0, st, x, \
+                                        rows, D, ldx, g, b, eps, yo, ldy)
+    if (nc <= 1) VTD_LN16(1);
+    else if (nc <= 2) VTD_LN16(2);
+    else VTD_LN16(4);
+#undef VTD_LN16
+    VTD_LAUNCH_CHECK("layernorm");
+    return VTD_OK;
+  }
   const int nv = (D + 255) / 256;
 #define VTD_LN(NV) hipLaunchKernelGGL((layernorm_kernel<TI, TO, NV>), grid, block, 0, st, x, rows, \
                                       D, ldx, g, b, eps, yo, ldy)
@@ -128,66 +301,75 @@ int ln_dispatch(const void* xv, int64_t rows, int D, int ldx, const float* g,
 }
 
 // LayerNorm with the output quantized to MX-fp8 (VTD_FP8 mode: the next GEMM's A operand
-// without a bf16 round trip through HBM).  Same statistics as layernorm_kernel; each lane
-// owns 4 consecutive columns, so a 32-column block is 8 consecutive lanes: block amax by
-// DPP (quad xor 1, xor 2) + one lane ^ 4 exchange; values are bf16-rounded first so the
-// bytes equal vtd_quantize_mx8 of layernorm_kernel's bf16 output.  NV covers Kq columns.
-template <typename TI, int NV>
+// without a bf16 round trip through HBM).  Same statistics as layernorm_kernel (same lane
+// layout and reduction order, so the same bits); each lane owns 4 consecutive columns, so a
+// 32-column block is 8 consecutive lanes: block amax by DPP (quad xor 1, xor 2) + one
+// lane ^ 4 exchange; values are bf16-rounded first so the bytes equal vtd_quantize_mx8 of
+// layernorm_kernel's bf16 output.  NV covers Kq columns.  RPW rows per wave, all their loads
+// issued before the first reduction (a read stream: the loads must be in flight together).
+template <typename TI, int NV, int RPW>
 __global__ __launch_bounds__(256) void layernorm_mx8_kernel(
     const TI* __restrict__ x, int64_t rows, int D, int ldx, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, uint8_t* __restrict__ q, int ldq, int Kq,
     uint8_t* __restrict__ sc, int64_t s_rows) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const TI* xr = x + row * ldx;
-  f32x4 v[NV];
-  float s = 0.f;
+  const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (row0 >= rows) return;
+  f32x4 v[RPW][NV];
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c = (i * 64 + lane) * 4;
-    v[i] = c < D ? ld4(xr + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-    s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
-  }
+  for (int r = 0; r < RPW; ++r) {
+    const TI* xr = x + min(row0 + r, rows - 1) * ldx;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  const float mean = s / D;
-  float qv = 0.f;
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c = (i * 64 + lane) * 4;
-    if (c < D)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float d = v[i][j] - mean;
-        qv += d * d;
-      }
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) qv += __shfl_xor(qv, o);
-  const float rstd = 1.f / sqrtf(qv / D + eps);
-  uint8_t* qr = q + row * ldq;
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c = (i * 64 + lane) * 4;
-    f32x4 o = {0.f, 0.f, 0.f, 0.f};
-    if (c < D) {
-      const f32x4 g = *reinterpret_cast<const f32x4*>(gamma + c);
-      const f32x4 bb = *reinterpret_cast<const f32x4*>(beta + c);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = bf16_round((v[i][j] - mean) * rstd * g[j] + bb[j]);
+    for (int i = 0; i < NV; ++i) {
+      const int c = (i * 64 + lane) * 4;
+      v[r][i] = c < D ? ld4(xr + c) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    float am = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3])));
-    am = fmaxf(am, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(am), 0xB1, 0xF, 0xF, false)));
-    am = fmaxf(am, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(am), 0x4E, 0xF, 0xF, false)));
-    am = fmaxf(am, __shfl_xor(am, 4));
-    const int E = mx8_exponent(am);
-    const float inv = __uint_as_float((uint32_t)(127 - E) << 23);
-    if (c < Kq) {
-      *reinterpret_cast<uint32_t*>(qr + c) = mx8_pack4(o[0], o[1], o[2], o[3], inv);
-      if ((lane & 7) == 0) {
-        const int b = c >> 5;
-        sc[((int64_t)(b >> 2) * s_rows + row) * 4 + (b & 3)] = (uint8_t)(E + 127);
+  }
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const int64_t row = row0 + r;
+    if (row >= rows) break;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) s += v[r][i][0] + v[r][i][1] + v[r][i][2] + v[r][i][3];
+    s = wave_sum(s);
+    const float mean = s / D;
+    float qv = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (i * 64 + lane) * 4;
+      if (c < D)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float d = v[r][i][j] - mean;
+          qv += d * d;
+        }
+    }
+    qv = wave_sum(qv);
+    const float rstd = 1.f / sqrtf(qv / D + eps);
+    uint8_t* qr = q + row * ldq;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (i * 64 + lane) * 4;
+      f32x4 o = {0.f, 0.f, 0.f, 0.f};
+      if (c < D) {
+        const f32x4 g = *reinterpret_cast<const f32x4*>(gamma + c);
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(beta + c);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = bf16_round((v[r][i][j] - mean) * rstd * g[j] + bb[j]);
+      }
+      float am = fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3])));
+      am = fmaxf(am, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(am), 0xB1, 0xF, 0xF, false)));
+      am = fmaxf(am, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(am), 0x4E, 0xF, 0xF, false)));
+      am = fmaxf(am, dpp_get<0x141>(am));   // row_half_mirror: the other quad
+      const int E = mx8_exponent(am);
+      const float inv = __uint_as_float((uint32_t)(127 - E) << 23);
+      if (c < Kq) {
+        *reinterpret_cast<uint32_t*>(qr + c) = mx8_pack4(o[0], o[1], o[2], o[3], inv);
+        if ((lane & 7) == 0) {
+          const int b = c >> 5;
+          sc[((int64_t)(b >> 2) * s_rows + row) * 4 + (b & 3)] = (uint8_t)(E + 127);
+        }
       }
     }
   }
@@ -238,8 +420,7 @@ __global__ __launch_bounds__(256) void ln_stats_kernel(const TI* __restrict__ x,
     for (int i = 0; i < NV; ++i)
 #pragma unroll
       for (int h = 0; h < 2; ++h) s += v[r][i][h][0] + v[r][i][h][1] + v[r][i][h][2] + v[r][i][h][3];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    s = wave_sum(s);
     const float mean = s / D;
     float q = 0.f;
 #pragma unroll
@@ -254,8 +435,7 @@ __global__ __launch_bounds__(256) void ln_stats_kernel(const TI* __restrict__ x,
             q += d * d;
           }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+    q = wave_sum(q);
     if (lane == 0 && row0 + r < rows) stat[row0 + r] = float2{mean, 1.f / sqrtf(q / D + eps)};
   }
 }
@@ -270,14 +450,14 @@ __global__ __launch_bounds__(256) void ln_stats_generic_kernel(const TI* __restr
   const TI* xr = x + row * ldx;
   float s = 0.f;
   for (int c = lane; c < D; c += 64) s += DT<TI>::load(xr + c);
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  s = wave_sum(s);
   const float mean = s / D;
   float q = 0.f;
   for (int c = lane; c < D; c += 64) {
     const float d = DT<TI>::load(xr + c) - mean;
     q += d * d;
   }
-  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+  q = wave_sum(q);
   if (lane == 0) stat[row] = float2{mean, 1.f / sqrtf(q / D + eps)};
 }
 
@@ -513,9 +693,30 @@ int layernorm_mx8_launch(const void* x, int x_dtype, int64_t rows, int D, int ld
                     reinterpret_cast<uintptr_t>(x) % (x_dtype == VTD_BF16 ? 8 : 16) == 0,
                 "layernorm_mx8: D, ldx % 4 and 16-B aligned gamma / beta / x needed");
   ProfScope ps(st, PROF_LN, 0.0);
-  const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  // rows per wave: 2 (the loads of both rows in flight)
+  constexpr int RPW = 2;
+  if (ln16_ok(x, x_dtype, D, ldx, g, b)) {
+    const dim3 g16((unsigned)((rows + 4 * RPW - 1) / (4 * RPW))), b16(256);
+    const int nc = (Kq + 1023) / 1024;
+#define VTD_LQ16(TI, NC) hipLaunchKernelGGL((layernorm16_mx8_kernel<TI, NC, RPW>), g16, b16, 0, st, \
+                                            static_cast<const TI*>(x), rows, D, ldx, g, b, eps, q, \
+                                            ldq, Kq, s, s_rows)
+    if (x_dtype == VTD_BF16) {
+      if (nc <= 1) VTD_LQ16(bf16_t, 1);
+      else if (nc <= 2) VTD_LQ16(bf16_t, 2);
+      else VTD_LQ16(bf16_t, 4);
+    } else {
+      if (nc <= 1) VTD_LQ16(float, 1);
+      else if (nc <= 2) VTD_LQ16(float, 2);
+      else VTD_LQ16(float, 4);
+    }
+#undef VTD_LQ16
+    VTD_LAUNCH_CHECK("layernorm_mx8");
+    return VTD_OK;
+  }
+  const dim3 grid((unsigned)((rows + 4 * RPW - 1) / (4 * RPW))), block(256);
   const int nv = (Kq + 255) / 256;
-#define VTD_LQ(TI, NV) hipLaunchKernelGGL((layernorm_mx8_kernel<TI, NV>), grid, block, 0, st,      \
+#define VTD_LQ(TI, NV) hipLaunchKernelGGL((layernorm_mx8_kernel<TI, NV, RPW>), grid, block, 0, st, \
                                           static_cast<const TI*>(x), rows, D, ldx, g, b, eps, q, \
                                           ldq, Kq, s, s_rows)
   if (x_dtype == VTD_BF16) {

@@ -863,6 +863,19 @@ __global__ __launch_bounds__(BNT) void gemm_mx8_pp_kernel(
 
 bool gemm_w4_launch(int M, int N, int K, const bf16_t* A, int lda, const bf16_t* Bt, int ldb,
                     const vtd_epilogue* epi, int ngw, hipStream_t stream);
+void gemm_mx8_x4_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_t* sA,
+                        int64_t sa_rows, const uint8_t* Bt, int ldb, const uint8_t* sB,
+                        int64_t sb_rows, const vtd_epilogue* epi, int ngw, hipStream_t stream);
+
+// The MX-fp8 kernel: 1 = the 8-wave ping-pong gemm_mx8_pp_kernel, 2 = x4 (vtd_gemm_w4.hip, one
+// wave per SIMD, persistent), 3 = x4 for K >= 2048 only.  VTD_MX_VARIANT (read per call) picks one; same products, same
+// epilogue arithmetic.
+constexpr int kDefaultMxVariant = 1;
+int mx_variant() {
+  const char* v = getenv("VTD_MX_VARIANT");
+  const int x = v ? atoi(v) : kDefaultMxVariant;
+  return (x >= 1 && x <= 3) ? x : kDefaultMxVariant;
+}
 
 // The bf16 256 x 256-tile kernel: 10 = pp2 (8-wave ping-pong, default), 12 = w4
 // (vtd_gemm_w4.hip, one wave per SIMD, persistent).  Both compute the same products with the
@@ -1056,6 +1069,13 @@ int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_
   ProfScope ps(stream, PROF_GEMM, flops > 0 ? flops : 2.0 * M * N * (double)K);
   const int tiles_m = (M + BBM - 1) / BBM, tiles_n = (N + BBN - 1) / BBN;
   e.ngw = tile_group_width(tiles_n);
+  // 3: x4 for the long-K layers (K >= 2048: the MLP's inner and last), ping-pong otherwise
+  const int mxv = mx_variant();
+  if (mxv == 2 || (mxv == 3 && K >= 2048)) {
+    gemm_mx8_x4_launch(M, N, K, A, lda, sA, sa_rows, Bt, ldb, sB, sb_rows, epi, e.ngw, stream);
+    VTD_LAUNCH_CHECK("gemm_mx8");
+    return VTD_OK;
+  }
   static std::once_flag once;
   std::call_once(once, [] {
 #define VTD_MX_FN(C) reinterpret_cast<const void*>(&gemm_mx8_pp_kernel<C>),

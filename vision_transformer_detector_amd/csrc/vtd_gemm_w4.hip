@@ -292,6 +292,19 @@ __device__ __forceinline__ f32x4 w4_acc(const f32x4& a) {
 // ops: the prologue's counted wait retires them, no load latency left in the epilogue)
 // EPI bit 16 (w4 only): the LayerNorm fold (epilogue.lnstat / colsum) is on
 constexpr int W4_LNFOLD = 16;
+// EPI bit 32 (the MX-fp8 x4 kernel only): MX-fp8 output (out_dtype VTD_FP8, e.sout scales)
+constexpr int W4_FP8OUT = 32;
+// max of v over lanes l, l ^ 16 (xmax16) / l, l ^ 32 (xmax32)
+__device__ __forceinline__ float xmax16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xmax32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
 template <int EPI>
 struct W4Cols {
   static constexpr int NC = (EPI & W4_LNFOLD) ? 4 : 1;
@@ -358,6 +371,7 @@ __device__ __forceinline__ void w4_epilogue_direct(const f32x4 (&acc)[8][8], int
   constexpr bool OUT_BF16 = (EPI & 4) != 0;
   constexpr bool RESID = (EPI & 8) != 0;
   constexpr int RW = W4Resid<EPI>::RW;
+  constexpr bool FP8OUT = (EPI & W4_FP8OUT) != 0;
   const int fr = lane & 15, fg = lane >> 4;
   // residual rows two row blocks ahead of their use (one wave per SIMD: nothing else hides
   // a load's latency); bf16: the first W4_RPRE preloaded by the caller
@@ -402,7 +416,29 @@ __device__ __forceinline__ void w4_epilogue_direct(const f32x4 (&acc)[8][8], int
       }
       if (e.out2) epi_out2_8(e, mrow, ncol, v0, v1);
       const int64_t idx = (int64_t)mrow * e.ldo + ncol;
-      if constexpr (OUT_BF16) {
+      if constexpr (FP8OUT) {
+        // the next MX GEMM's operand: the 32-column block 32 jp .. + 31 of this row is held
+        // by lanes fr + 16 g (g = 0..3, 8 columns each): block amax by the two lane swaps,
+        // of bf16-rounded values (bytes = vtd_quantize_mx8 of the bf16 output)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v0[j] = bf16_round(v0[j]);
+          v1[j] = bf16_round(v1[j]);
+        }
+        float am = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) am = fmaxf(am, fmaxf(fabsf(v0[j]), fabsf(v1[j])));
+        am = xmax32(xmax16(am));
+        const int E = mx8_exponent(am);
+        const float inv = __uint_as_float((uint32_t)(127 - E) << 23);
+        const uint2 qv = {mx8_pack4(v0[0], v0[1], v0[2], v0[3], inv),
+                          mx8_pack4(v1[0], v1[1], v1[2], v1[3], inv)};
+        *reinterpret_cast<uint2*>(static_cast<uint8_t*>(e.out) + idx) = qv;
+        if (fg == 0) {
+          const int b = (n_base + 32 * jp) >> 5;
+          e.sout[((int64_t)(b >> 2) * e.s_rows + mrow) * 4 + (b & 3)] = (uint8_t)(E + 127);
+        }
+      } else if constexpr (OUT_BF16) {
         const i32x4 o = {(int)pack_bf16x2(v0[0], v0[1]), (int)pack_bf16x2(v0[2], v0[3]),
                          (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
         store_out16(static_cast<bf16_t*>(e.out) + idx, o);
@@ -414,7 +450,7 @@ __device__ __forceinline__ void w4_epilogue_direct(const f32x4 (&acc)[8][8], int
         *reinterpret_cast<f32x4*>(op + 4) = v1;
       }
     }
-    if (OUT_BF16 && e.statout) {
+    if (OUT_BF16 && !FP8OUT && e.statout) {
       // LayerNorm partials of the two 64-column blocks: a block's 64 values of this row are
       // in lanes fr, fr + 16, + 32, + 48 (jp = 2 b, 2 b + 1)
 #pragma unroll
@@ -566,6 +602,358 @@ int w4_sched() {
   return v && atoi(v) == 2 ? 2 : 1;
 }
 
+
+// ============================================================================
+// "x4": the MX-fp8 GEMM (VTD_FP8 mode) on the w4 structure: A, Bt are
+// OCP e4m3 bytes with one E8M0 scale per 32 K-elements (vtd_mx8.hip layout: scales
+// s[k / 128][rows][4]); D += A Bt^T by v_mfma_scale_f32_16x16x128_f8f6f4.  One wave per
+// SIMD, tile 256 x 256, K-step 128 elements = 128 B per row (the bf16 w4 staging byte for
+// byte) + 1 KiB of A scales and 1 KiB of B scales per stage (lanes 0-15 of each wave DMA
+// 256 B of each).  Accumulators, B-row permutation and the epilogues are w4's.
+//
+// A scaled MFMA consumes a whole K-step of both operands (32 B per lane: chunks fg and
+// 4 + fg of the row, scale byte fg -- the convention the ping-pong MX kernel measured), so
+// w4's double-buffered half-K-step fragments do not exist here.  Instead the wave's 128 x 128
+// block is four quadrants of 16 MFMAs over operand halves A0 / A1 (row blocks 0-3 / 4-7)
+// and B0 / B1 (column blocks 0-3 / 4-7), 4 x 36 VGPRs in all, walked in a zig-zag so that
+// every half is re-read one or two quadrants before its next use:
+//   K-step t, bf = the B half step t starts with (t even: B0, odd: B1), bs = the other:
+//     q0 (A0, bf): read bs(t), A1(t)
+//     q1 (A0, bs)
+//     lgkmcnt(0); vmcnt(0); barrier     stage t & 1 read by every wave (WAR for tile t + 2),
+//                                       tile t + 1 landed (RAW)
+//     q2 (A1, bs): read A0(t + 1); DMA tile t + 2 -> stage t & 1
+//     q3 (A1, bf): read bs(t + 1)      (= the half step t + 1 starts with)
+// ============================================================================
+constexpr int X4_SCL = 1024;                       // one operand's scales of a K-step
+constexpr int X4_STAGE = 2 * W4_OPND + 2 * X4_SCL; // 66 KiB
+constexpr int X4_LDS = 2 * X4_STAGE;               // 132 KiB
+
+struct X4Src {
+  __amdgpu_buffer_rsrc_t ra, rb, rsa, rsb, nul;   // nul: no records (every access out of range)
+  int va, vb0, vb1;   // per lane: row lane >> 3 of a DMA piece + its swizzled chunk (B: pieces
+                      // j with bit 1 of j clear / set)
+  int vsa, vsb;       // per lane: the scale dword of row 64 w + l in a K-step
+  int pa, pb;         // wave-uniform: bytes from the tile base to the wave's first row
+  int lda, ldb, sa4, sb4;
+};
+
+// Rows past the matrix read as zero (out of the records: no clamping, no per-piece offsets)
+__device__ __forceinline__ void x4_sources(X4Src& s, const uint8_t* A, int lda, int M,
+                                           const uint8_t* sA, int64_t sa_rows, const uint8_t* Bt,
+                                           int ldb, int N, const uint8_t* sB, int64_t sb_rows,
+                                           int K, int m0, int n0, int wave, int lane) {
+  const int64_t ra_bytes = (int64_t)(M - m0) * lda, rb_bytes = (int64_t)(N - n0) * ldb;
+  s.ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(A + (int64_t)m0 * lda), 0,
+                                           (int)std::min<int64_t>(ra_bytes, 0x7fffffff), 0x00020000);
+  s.rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(Bt + (int64_t)n0 * ldb), 0,
+                                           (int)std::min<int64_t>(rb_bytes, 0x7fffffff), 0x00020000);
+  // scale rows past sa_rows / sb_rows fall outside the records (read as zero; never stored)
+  s.rsa = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sA), 0,
+                                            (int)std::min<int64_t>(sa_rows * K / 32, 0x7fffffff), 0x00020000);
+  s.rsb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sB), 0,
+                                            (int)std::min<int64_t>(sb_rows * K / 32, 0x7fffffff), 0x00020000);
+  s.nul = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sA), 0, 0, 0x00020000);
+  const int prow = lane >> 3, c = lane & 7;
+  s.va = prow * lda + ((c ^ prow) << 4);
+  s.vb0 = prow * ldb + ((c ^ prow) << 4);
+  s.vb1 = prow * ldb + ((c ^ prow ^ 4) << 4);
+  s.vsa = (m0 + wave * 64 + lane) * 4;
+  s.vsb = (n0 + wave * 64 + lane) * 4;
+  s.pa = wave * 64 * lda;
+  s.pb = wave * 64 * ldb;
+  s.lda = lda;
+  s.ldb = ldb;
+  s.sa4 = (int)(sa_rows * 4);
+  s.sb4 = (int)(sb_rows * 4);
+}
+
+// DMA piece j (rows 64 w + 8 j .. + 7) of K-step kt of both operands; live = false: the
+// same instructions against the empty descriptor (the loop's tail K-steps: nothing is read)
+__device__ __forceinline__ void x4_dma(char* stage, const X4Src& s, int wave, int kt, int j,
+                                       bool live = true) {
+  char* da = stage + wave * 64 * 128 + j * 1024;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(live ? s.ra : s.nul, (w4_lds_t*)da, 16, s.va,
+                                           s.pa + 8 * j * s.lda + kt * 128, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(live ? s.rb : s.nul, (w4_lds_t*)(da + W4_OPND), 16,
+                                           ((j >> 1) & 1) ? s.vb1 : s.vb0,
+                                           s.pb + 8 * j * s.ldb + kt * 128, 0, 0);
+}
+// the wave's 64 rows of A and B scales of K-step kt (one dword = one row per lane)
+__device__ __forceinline__ void x4_dma_scales(char* stage, const X4Src& s, int wave, int kt,
+                                              bool live = true) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(live ? s.rsa : s.nul,
+                                           (w4_lds_t*)(stage + 2 * W4_OPND + wave * 256), 4, s.vsa,
+                                           kt * s.sa4, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(live ? s.rsb : s.nul,
+                                           (w4_lds_t*)(stage + 2 * W4_OPND + X4_SCL + wave * 256),
+                                           4, s.vsb, kt * s.sb4, 0, 0);
+}
+
+typedef __attribute__((ext_vector_type(8))) int x4_i32x8;
+// one operand half: 4 blocks x 32 B (chunks fg and 4 + fg of the row: one MFMA operand) +
+// the lane's scale byte of each block's row
+struct X4Half {
+  x4_i32x8 v[4];
+  int s[4];
+};
+// per-lane LDS offsets (block offsets are immediates)
+struct X4Offs {
+  int a0, a1;               // A row wm * 128 + fr: chunk fg / 4 + fg
+  int b00, b01, b10, b11;   // B rows perm(0 / 1, fr): chunk fg (b0*) / 4 + fg (b1*)
+  int sa, sb0, sb1;         // scale byte fg of A row wm * 128 + fr / B rows perm(0 / 1, fr)
+};
+template <int H>
+__device__ __forceinline__ void x4_read_a(X4Half& h, const char* st, const X4Offs& o) {
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int i = 4 * H + b;
+    h.v[b].lo = *reinterpret_cast<const i32x4*>(st + o.a0 + i * 16 * 128);
+    h.v[b].hi = *reinterpret_cast<const i32x4*>(st + o.a1 + i * 16 * 128);
+    h.s[b] = *reinterpret_cast<const uint8_t*>(st + 2 * W4_OPND + o.sa + i * 16 * 4);
+  }
+}
+template <int H>
+__device__ __forceinline__ void x4_read_b(X4Half& h, const char* st, const X4Offs& o) {
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int j = 4 * H + b;
+    const int blk = (j >> 1) * 32;
+    h.v[b].lo = *reinterpret_cast<const i32x4*>(st + W4_OPND + ((j & 1) ? o.b01 : o.b00) + blk * 128);
+    h.v[b].hi = *reinterpret_cast<const i32x4*>(st + W4_OPND + ((j & 1) ? o.b11 : o.b10) + blk * 128);
+    h.s[b] = *reinterpret_cast<const uint8_t*>(st + 2 * W4_OPND + X4_SCL +
+                                               ((j & 1) ? o.sb1 : o.sb0) + blk * 4);
+  }
+}
+// one MFMA row of a quadrant: output row block 4 HA + i, column blocks 4 HB .. 4 HB + 3
+// (operands swapped as in w4: D = B-block x A-block^T; scale A = the B rows', scale B = the
+// A rows').  Inline asm with the accumulator tied in place ("+a"): the builtin's AGPR form
+// has no tied-accumulator variant, so the compiler rotates every result through a
+// temporary quad with 4 copies and a 7-cycle hazard NOP per MFMA.  Hazards the compiler
+// then no longer sees: a block's next accumulation is >= 16 MFMAs later, nothing but these
+// instructions writes the accumulators in the K loop, and x4_mainloop ends with the
+// wait states an MFMA result needs before the epilogue's AGPR reads.
+template <int HA, int HB>
+__device__ __forceinline__ void x4_mfma_row(f32x4 (&acc)[8][8], const X4Half& a, const X4Half& b,
+                                            int i) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel_hi:[0,0,0]"
+                 : "+a"(acc[4 * HA + i][4 * HB + j])
+                 : "v"(b.v[j]), "v"(a.v[i]), "v"(b.s[j]), "v"(a.s[i]));
+}
+
+// K-step t (stage t & 1 holds tile t; a0 and bf, the B half (index HF) step t starts with,
+// hold tile t).  Tile t + 2 is DMA'd when it exists (else the empty descriptor); tile t + 1's
+// first halves are read into a0 and bs (B half HS: the half step t + 1 starts with; stale
+// stage bytes after the last K-step, never used).  The caller swaps bf / bs every step.
+// SCHED 1: one barrier (before q2), tile t + 2's DMA during q2 / q3 (one K-step to land).
+// SCHED 2: a first barrier after q0 (stage t read by every wave: its DMA starts in q1) and
+// the second before q2 (tile t + 1 landed: vmcnt counts the 6 DMAs issued in q1): 1.25
+// K-steps to land.
+template <int HF, int DG, int SCHED>
+__device__ __forceinline__ void x4_kstep(f32x4 (&acc)[8][8], X4Half& a0, X4Half& a1, X4Half& bf,
+                                         X4Half& bs, char* smem, const X4Src& src, int t, int nk,
+                                         int wave, int lane, const X4Offs& o) {
+  constexpr int HS = 1 - HF;
+  char* st = smem + (t & 1) * X4_STAGE;
+  const char* nx = smem + ((t + 1) & 1) * X4_STAGE;
+  const bool pf = t + 2 < nk && !(DG & 1);
+  w4_fence();
+  // q0 (A0, bf): read bs(t), A1(t)
+  x4_read_b<HS>(bs, st, o);
+  x4_read_a<1>(a1, st, o);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) x4_mfma_row<0, HF>(acc, a0, bf, i);
+  w4_fence();
+  if constexpr (SCHED == 2) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    w4_barrier();                                     // stage t free
+    x4_dma_scales(st, src, wave, t + 2, pf);
+  }
+  // q1 (A0, bs)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (SCHED == 2 && i < 2) x4_dma(st, src, wave, t + 2, i, pf);
+    x4_mfma_row<0, HS>(acc, a0, bs, i);
+    w4_fence();
+  }
+  if constexpr (SCHED == 2) {
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // tile t + 1 (older than q1's 6)
+  } else {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile t + 1 (the only DMA in flight)
+  }
+  w4_barrier();
+  // q2 (A1, bs): read A0(t + 1), DMA tile t + 2
+  x4_read_a<0>(a0, nx, o);
+  if (SCHED == 1) x4_dma_scales(st, src, wave, t + 2, pf);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (SCHED == 1) x4_dma(st, src, wave, t + 2, i, pf);
+    else if (i < 3) x4_dma(st, src, wave, t + 2, 2 + i, pf);
+    x4_mfma_row<1, HS>(acc, a1, bs, i);
+    w4_fence();
+  }
+  // q3 (A1, bf): read bs(t + 1) (bs's last use was q2)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (SCHED == 1) x4_dma(st, src, wave, t + 2, 4 + i, pf);
+    else if (i < 3) x4_dma(st, src, wave, t + 2, 5 + i, pf);
+    if (i == 0) x4_read_b<HS>(bs, nx, o);
+    x4_mfma_row<1, HF>(acc, a1, bf, i);
+    w4_fence();
+  }
+}
+
+// K-tiles 0 and 1 of a tile into stages 0 and 1 (the stages must be free)
+__device__ __forceinline__ void x4_issue_k01(char* smem, const X4Src& src, int wave, int lane,
+                                             int nk) {
+  x4_dma_scales(smem, src, wave, 0);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x4_dma(smem, src, wave, 0, j);
+  if (nk > 1) {
+    x4_dma_scales(smem + X4_STAGE, src, wave, 1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x4_dma(smem + X4_STAGE, src, wave, 1, j);
+  }
+}
+
+template <int DG, int SCHED>
+__device__ __forceinline__ void x4_mainloop(f32x4 (&acc)[8][8], char* smem, const X4Src& src,
+                                            int nk, int wave, int wm, int wn, int lane) {
+  const int fr = lane & 15, fg = lane >> 4;
+  X4Offs o;
+  o.a0 = w4_swz_a(wm * 128 + fr, fg);
+  o.a1 = w4_swz_a(wm * 128 + fr, 4 + fg);
+  const int brow0 = wn * 128 + w4_perm(0, fr), brow1 = wn * 128 + w4_perm(1, fr);
+  o.b00 = w4_swz_b(brow0, fg);
+  o.b01 = w4_swz_b(brow1, fg);
+  o.b10 = w4_swz_b(brow0, 4 + fg);
+  o.b11 = w4_swz_b(brow1, 4 + fg);
+  o.sa = 4 * (wm * 128 + fr) + fg;
+  o.sb0 = 4 * brow0 + fg;
+  o.sb1 = 4 * brow1 + fg;
+  // K-tile 0 retired (K-tile 1's DMA, or more, is younger), every wave's part visible
+  if (nk > 1) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  w4_barrier();
+  asm volatile("s_nop 4" ::: "memory");            // accumulator init -> first MFMA srcC
+  X4Half a0, a1, b0, b1;
+  x4_read_a<0>(a0, smem, o);
+  x4_read_b<0>(b0, smem, o);
+  // even steps start with B half 0 (bf = b0), odd steps with B half 1 (bf = b1)
+  int t = 0;
+  for (; t + 1 < nk; t += 2) {
+    x4_kstep<0, DG, SCHED>(acc, a0, a1, b0, b1, smem, src, t, nk, wave, lane, o);
+    x4_kstep<1, DG, SCHED>(acc, a0, a1, b1, b0, smem, src, t + 1, nk, wave, lane, o);
+  }
+  if (t < nk) x4_kstep<0, DG, SCHED>(acc, a0, a1, b0, b1, smem, src, t, nk, wave, lane, o);
+  // the last MFMAs' results: wait states before any AGPR read (XDL write -> VALU read)
+  asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+}
+
+// Persistent like the w4 kernel (the next tile's K-tiles 0 and 1 are DMA'd during the
+// current tile's register-direct epilogue).
+// DG (VTD_DIAG builds only; timing diagnostics, WRONG outputs): bit 0 = no DMA after a tile's
+// first two K-tiles (the K loop reads stale stages), bit 1 = no epilogue (nothing stored)
+template <int EPI, int SCHED, int DG = 0>
+__global__ __launch_bounds__(W4_T, 1) void gemm_mx8_x4_kernel(
+    int M, int N, int K, const uint8_t* __restrict__ A, int lda, const uint8_t* __restrict__ sA,
+    int64_t sa_rows, const uint8_t* __restrict__ Bt, int ldb, const uint8_t* __restrict__ sB,
+    int64_t sb_rows, int tiles_m, int tiles_n, EpiArgs e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int T = tiles_m * tiles_n, G = gridDim.x, nk = K / 128;
+  int vb = blockIdx.x;
+  if (vb >= T) return;
+  int m0, n0;
+  w4_tile(vb, tiles_m, tiles_n, e.ngw, m0, n0);
+  X4Src src;
+  x4_sources(src, A, lda, M, sA, sa_rows, Bt, ldb, N, sB, sb_rows, K, m0, n0, wave, lane);
+  x4_issue_k01(smem, src, wave, lane, nk);
+  for (;;) {
+    const int m_base = m0 + wm * 128, n_base = n0 + wn * 128;
+    const bool full = m0 + W4_TILE <= M && n0 + W4_TILE <= N;
+    W4Cols<EPI> cols;
+    if constexpr (EPI != EPI_GENERIC) {
+      if (full) w4_load_cols(cols, e, n_base, lane);
+    }
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    x4_mainloop<DG, SCHED>(acc, smem, src, nk, wave, wm, wn, lane);
+    const int vn = vb + G;
+    const bool more = vn < T;
+    int m1 = 0, n1 = 0;
+    if (more) w4_tile(vn, tiles_m, tiles_n, e.ngw, m1, n1);
+    if constexpr (DG & 2) {
+      if (!more) return;
+      vb = vn;
+      m0 = m1;
+      n0 = n1;
+      x4_sources(src, A, lda, M, sA, sa_rows, Bt, ldb, N, sB, sb_rows, K, m0, n0, wave, lane);
+      x4_issue_k01(smem, src, wave, lane, nk);
+      continue;
+    }
+    if constexpr (EPI != EPI_GENERIC) {
+      if (full) {
+        W4Resid<EPI> rr;
+        if constexpr (w4_resid_preloaded<EPI>()) {
+#pragma unroll
+          for (int i = 0; i < W4_RPRE; ++i) w4_load_resid<EPI>(rr, e, lane, m_base, n_base, i);
+        }
+        w4_epilogue_direct<EPI>(acc, lane, m_base, n_base, e, nullptr, cols, rr, [&] {
+          if (more) {
+            x4_sources(src, A, lda, M, sA, sa_rows, Bt, ldb, N, sB, sb_rows, K, m1, n1, wave,
+                       lane);
+            x4_issue_k01(smem, src, wave, lane, nk);
+          }
+        });
+        if (!more) return;
+        vb = vn;
+        m0 = m1;
+        n0 = n1;
+        continue;
+      }
+    }
+    w4_epilogue_generic(acc, reinterpret_cast<float*>(smem) + wave * 32 * W4_ES, lane, M, N,
+                        m_base, n_base, e);
+    if (!more) return;
+    w4_fence();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    w4_barrier();
+    vb = vn;
+    m0 = m1;
+    n0 = n1;
+    x4_sources(src, A, lda, M, sA, sa_rows, Bt, ldb, N, sB, sb_rows, K, m0, n0, wave, lane);
+    x4_issue_k01(smem, src, wave, lane, nk);
+  }
+}
+
+template <int C, int SCHED, int DG = 0>
+void x4_launch(dim3 g, hipStream_t stream, int M, int N, int K, const uint8_t* A, int lda,
+               const uint8_t* sA, int64_t sa_rows, const uint8_t* Bt, int ldb, const uint8_t* sB,
+               int64_t sb_rows, int tiles_m, int tiles_n, const EpiArgs& e) {
+  static std::once_flag once[kMaxDevices];
+  once_per_device(once, [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_mx8_x4_kernel<C, SCHED, DG>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, X4_LDS);
+  });
+  hipLaunchKernelGGL((gemm_mx8_x4_kernel<C, SCHED, DG>), g, dim3(W4_T), X4_LDS, stream, M, N, K, A, lda, sA,
+                     sa_rows, Bt, ldb, sB, sb_rows, tiles_m, tiles_n, e);
+}
+// x4 K-step schedule (VTD_X4_SCHED, read per call; both exact): 1 = one barrier per K-step,
+// 2 = two (the next-but-one K-tile's DMA starts a quadrant earlier)
+int x4_sched() {
+  const char* v = getenv("VTD_X4_SCHED");
+  return v && atoi(v) == 1 ? 1 : 2;
+}
+
 }  // namespace
 
 // The w4 GEMM for a bf16 problem (the caller checked shapes / dtypes and finalized any
@@ -597,6 +985,7 @@ bool gemm_w4_launch(int M, int N, int K, const bf16_t* A, int lda, const bf16_t*
     return true;
   }
 #endif
+#ifndef VTD_X4_ONLY   // (build-speed aid for the x4 kernel's register tuning)
   const int sched = w4_sched();
   switch (code) {
 #define VTD_W4_CASE(C)                                                                       \
@@ -613,7 +1002,68 @@ bool gemm_w4_launch(int M, int N, int K, const bf16_t* A, int lda, const bf16_t*
       if (sched == 2) w4_launch<EPI_GENERIC, 2>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
       else w4_launch<EPI_GENERIC, 1>(g, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
   }
+#endif
   return true;
+}
+
+// The x4 MX-fp8 GEMM (the caller checked shapes and the fp8-output conditions).
+void gemm_mx8_x4_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_t* sA,
+                        int64_t sa_rows, const uint8_t* Bt, int ldb, const uint8_t* sB,
+                        int64_t sb_rows, const vtd_epilogue* epi, int ngw, hipStream_t stream) {
+  EpiArgs e = make_epi_args(epi);
+  e.ngw = ngw;
+  auto a16 = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
+  const bool fast = e.bias && !e.dets && !e.lnstat && e.scatter_tokens <= 0 && e.ldo % 8 == 0 &&
+                    (!e.resid || e.ldr % 8 == 0) && a16(e.out) && a16(e.bias) &&
+                    (!e.resid || a16(e.resid)) && (!e.out2 || (e.ldo2 % 8 == 0 && a16(e.out2)));
+  const bool fp8out = e.out_dtype == VTD_FP8;
+  const int code = fast ? epi_code(e.act, e.out_dtype != VTD_F32, e.resid != nullptr) |
+                              (fp8out ? W4_FP8OUT : 0)
+                        : EPI_GENERIC;
+  const int tiles_m = (M + W4_TILE - 1) / W4_TILE, tiles_n = (N + W4_TILE - 1) / W4_TILE;
+  const dim3 g(std::min(tiles_m * tiles_n, device_cu_count()));
+  const int sched = x4_sched();
+#if VTD_DIAG
+  // timing diagnostics (wrong outputs), plain bf16 epilogue only: VTD_X4_DG = 1 / 2 / 3
+  if (const char* dg = getenv("VTD_X4_DG"); dg && atoi(dg) > 0 && code == 4) {
+    const int d = atoi(dg);
+    if (d == 1) x4_launch<4, 1, 1>(g, stream, M, N, K, A, lda, sA, sa_rows, Bt, ldb, sB, sb_rows, tiles_m, tiles_n, e);
+    else if (d == 2) x4_launch<4, 1, 2>(g, stream, M, N, K, A, lda, sA, sa_rows, Bt, ldb, sB, sb_rows, tiles_m, tiles_n, e);
+    else x4_launch<4, 1, 3>(g, stream, M, N, K, A, lda, sA, sa_rows, Bt, ldb, sB, sb_rows, tiles_m, tiles_n, e);
+    return;
+  }
+#endif
+#ifdef VTD_X4_ONLY
+  if (code == 4) {
+    if (x4_sched() == 2) x4_launch<4, 2>(g, stream, M, N, K, A, lda, sA, sa_rows, Bt, ldb, sB, sb_rows, tiles_m, tiles_n, e);
+    else x4_launch<4, 1>(g, stream, M, N, K, A, lda, sA, sa_rows, Bt, ldb, sB, sb_rows, tiles_m, tiles_n, e);
+    return;
+  }
+#endif
+  switch (code) {
+#define VTD_X4_CASE(C)                                                                     \
+  case C:                                                                                  \
+    if (sched == 2)                                                                        \
+      x4_launch<C, 2>(g, stream, M, N, K, A, lda, sA, sa_rows, Bt, ldb, sB, sb_rows,       \
+                      tiles_m, tiles_n, e);                                                \
+    else                                                                                   \
+      x4_launch<C, 1>(g, stream, M, N, K, A, lda, sA, sa_rows, Bt, ldb, sB, sb_rows,       \
+                      tiles_m, tiles_n, e);                                                \
+    break;
+#ifndef VTD_X4_ONLY
+    VTD_X4_CASE(0) VTD_X4_CASE(1) VTD_X4_CASE(2) VTD_X4_CASE(4) VTD_X4_CASE(5) VTD_X4_CASE(6)
+    VTD_X4_CASE(8) VTD_X4_CASE(9) VTD_X4_CASE(10) VTD_X4_CASE(12) VTD_X4_CASE(13)
+    VTD_X4_CASE(14) VTD_X4_CASE(36) VTD_X4_CASE(37) VTD_X4_CASE(38)
+#endif
+#undef VTD_X4_CASE
+    default:
+      if (sched == 2)
+        x4_launch<EPI_GENERIC, 2>(g, stream, M, N, K, A, lda, sA, sa_rows, Bt, ldb, sB, sb_rows,
+                                  tiles_m, tiles_n, e);
+      else
+        x4_launch<EPI_GENERIC, 1>(g, stream, M, N, K, A, lda, sA, sa_rows, Bt, ldb, sB, sb_rows,
+                                  tiles_m, tiles_n, e);
+  }
 }
 
 }  // namespace vtd
