@@ -44,7 +44,8 @@ def test_removed_switches_are_not_read_by_the_library(L):
     from the product library: their names are not in libvtd.so's strings, so no getenv can
     read them (the GPU test checks the logits with them set)."""
     blob = open(L.lib._name, "rb").read()
-    for name in (b"VTD_ATTN_DIAG", b"VTD_PP3_DIAG", b"VTD_LN_FUSE", b"VTD_W4_DG"):
+    for name in (b"VTD_ATTN_DIAG", b"VTD_PP3_DIAG", b"VTD_LN_FUSE", b"VTD_W4_DG",
+                 b"VTD_DIAG_NOFIN", b"VTD_DIAG_NOATTN", b"VTD_DIAG_NOHEAD"):
         assert name + b"\0" not in blob, name
     assert b"VTD_GEMM_VARIANT\0" in blob   # the live A/B switch: 10 (default) or 12
 

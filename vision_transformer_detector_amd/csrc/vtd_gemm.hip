@@ -992,8 +992,8 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
       VTD_LAUNCH_CHECK("gemm");
       return VTD_OK;
     }
-    static std::once_flag once;
-    std::call_once(once, [] {
+    static std::once_flag once[kMaxDevices];
+    once_per_device(once, [] {
 #define VTD_PP_FN(C) reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, false>), \
                      reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, true>),
       const void* fns[] = {VTD_PP_FN(EPI_GENERIC) VTD_PP_FN(0) VTD_PP_FN(1) VTD_PP_FN(2)
@@ -1076,8 +1076,8 @@ int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_
     VTD_LAUNCH_CHECK("gemm_mx8");
     return VTD_OK;
   }
-  static std::once_flag once;
-  std::call_once(once, [] {
+  static std::once_flag once[kMaxDevices];
+  once_per_device(once, [] {
 #define VTD_MX_FN(C) reinterpret_cast<const void*>(&gemm_mx8_pp_kernel<C>),
     const void* fns[] = {VTD_MX_FN(EPI_GENERIC) VTD_MX_FN(0) VTD_MX_FN(1) VTD_MX_FN(2)
                          VTD_MX_FN(4) VTD_MX_FN(5) VTD_MX_FN(6) VTD_MX_FN(8) VTD_MX_FN(9)

@@ -443,7 +443,16 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     partials = gemm_emits_stats(M, Dp, dt, &e);
     if (!partials) { e.statout = nullptr; e.stat_ld = 0; }
   };
+#ifndef VTD_DIAG
+#define VTD_DIAG 0
+#endif
+  // VTD_DIAG builds only (timing diagnostics, WRONG outputs): VTD_DIAG_NOFIN skips the
+  // LayerNorm finalize launches, VTD_DIAG_NOATTN the attention launches, VTD_DIAG_NOHEAD
+  // the detection head
+  static const bool diag_nofin = VTD_DIAG && getenv("VTD_DIAG_NOFIN");
+  static const bool diag_noattn = VTD_DIAG && getenv("VTD_DIAG_NOATTN");
   auto row_stats = [&]() -> int {
+    if (diag_nofin) return VTD_OK;
     return partials ? ln_stats_finalize_launch(pstat, R, nslot, D, 1e-3f, stat, st)
                     : ln_stats_launch(x, rdt, R, D, Dp, 1e-3f, stat, st);
   };
@@ -539,7 +548,8 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     // VTD_FP8 with whole MX K-steps: attention writes the output GEMM's MX-fp8 operand
     const bool attn_mx8 = fp8 && d.inner_p % 128 == 0 && k8_of(d.inner_p) == d.inner_p;
     const double attn_flops = 4.0 * B * cfg->num_heads * (double)N * N * cfg->key_dim;
-    rc = attn_mx8 ? attention_mx8_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale,
+    rc = diag_noattn ? VTD_OK
+         : attn_mx8 ? attention_mx8_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale,
                                          q8, d.inner_p, s8, P.s8_rows, st, attn_flops)
                   : attention_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale,
                                      attn, d.inner_p, dt, st, attn_flops);
@@ -610,6 +620,8 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     }
   }
   if (!(s_lo <= n_stages - 1 && n_stages - 1 < s_hi)) return VTD_OK;
+  static const bool diag_nohead = VTD_DIAG && getenv("VTD_DIAG_NOHEAD");
+  if (diag_nohead) return VTD_OK;
   // ---- mlp_head: Dense(17) + Reshape((17, -1)) as a scatter epilogue (vtd.py:454-463)
   {
     const size_t es = es_of(dt);
