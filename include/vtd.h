@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define VTD_ABI_VERSION 11
+#define VTD_ABI_VERSION 12
 #define VTD_KALIGN 64          /* K / row padding granule, elements              */
 #define VTD_MAX_MLP 16         /* max encoder_mlp_quantities                     */
 #define VTD_MAX_HEAD 64        /* max mlp_head layers * repeats                   */
@@ -195,6 +195,28 @@ typedef struct vtd_epilogue {
 } vtd_epilogue;
 int vtd_gemm(int M, int N, int K, const void* A_dev, int lda, const void* Bt_dev,
              int ldb, int dtype, const vtd_epilogue* epi, void* stream);
+/* Split-K form of vtd_gemm (bf16 only; what vtd_forward runs for the detection head's
+ * few-tile, long-K Dense layers, vtd.py:468-486): `ksplit` K ranges of K / 64 / ksplit
+ * K-steps each write fp32 partial sums into part_dev ([ksplit][M][N] floats,
+ * part_bytes >= ksplit * M * N * 4), then one pass sums them in split order and applies
+ * the epilogue (no LayerNorm fold / statistics).  K % 64 == 0, N % 4 == 0,
+ * 2 <= ksplit <= K / 64 with every split non-empty.  vtd_gemm_splitk_choice returns the
+ * split count vtd_forward uses for (M, N, K, dtype) (1 = no split). */
+int vtd_gemm_splitk(int M, int N, int K, const void* A_dev, int lda, const void* Bt_dev,
+                    int ldb, const vtd_epilogue* epi, float* part_dev, size_t part_bytes,
+                    int ksplit, void* stream);
+int vtd_gemm_splitk_choice(int M, int N, int K, int dtype);
+/* vtd_gemm for a folded LayerNorm whose row statistics are still a producer's centred
+ * partials (`statout` layout: lnslots (block mean, M2) pairs per row, D = 64 * lnslots,
+ * eps): what vtd_forward runs for the query/key/value and first-MLP GEMMs.  Where the
+ * 256-tile bf16 kernel serves every tile on its fast epilogues (M % 256 == N % 256 == 0,
+ * lnslots 12 or 16, lnpart 16-B aligned) it merges each row's partials itself (Chan, the
+ * arithmetic of vtd_layernorm_stats_finalize) and epi->lnstat is not written; otherwise
+ * vtd_layernorm_stats_finalize writes epi->lnstat first.  VTD_LN_FINALIZE=1 forces the
+ * latter (read per call). */
+int vtd_gemm_ln(int M, int N, int K, const void* A_dev, int lda, const void* Bt_dev, int ldb,
+                int dtype, const vtd_epilogue* epi, const float* lnpart_dev, int lnslots,
+                int lnD, float lneps, void* stream);
 
 /* MX-fp8 operands (OCP MX: e4m3 elements, one E8M0 scale byte e = 2^(e-127) per 32
  * consecutive K elements).  vtd_quantize_mx8: x [rows][ldx] (x_dtype F32 or BF16), first

@@ -631,3 +631,112 @@ def test_gemm_statout_unsupported_shape(L, cuda):
     with pytest.raises(L.VtdError):
         L.check(L.lib.vtd_gemm(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, L.BF16, ctypes.byref(e),
                                L.stream_ptr()), "gemm")
+
+
+@pytest.mark.parametrize("M,N,K,ksplit,act,out_dtype", [
+    (2176, 4352, 8704, 2, 1, 1), (2176, 2176, 4352, 4, 1, 1), (2176, 1088, 2176, 4, 2, 1),
+    (300, 520, 1088, 3, 0, 0), (1000, 136, 640, 5, 1, 0), (257, 264, 192, 3, 0, 1)])
+def test_gemm_splitk(L, cuda, M, N, K, ksplit, act, out_dtype):
+    """vtd_gemm_splitk (the head's few-tile, long-K layers): fp32 partial sums of ksplit K
+    ranges summed in split order + the epilogue, against fp64 and within fp32 summation-order
+    noise of the unsplit kernel; ragged M / N take the masked partial tiles."""
+    g = torch.Generator(device=cuda).manual_seed(M + N + K + ksplit)
+    A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
+    Bt = (torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g, device=cuda)
+    resid = torch.randn(M, N, generator=g, device=cuda) if out_dtype == 0 else None
+    odt = torch.float32 if out_dtype == 0 else torch.bfloat16
+    out = torch.full((M, N), float("nan"), device=cuda, dtype=odt)
+    part = torch.full((ksplit, M, N), float("nan"), device=cuda)
+    e = L.VtdEpilogue()
+    e.bias, e.act, e.out, e.ldo, e.out_dtype = L.ptr(bias), act, L.ptr(out), N, out_dtype
+    e.resid, e.ldr = L.ptr(resid), (N if resid is not None else 0)
+    L.check(L.lib.vtd_gemm_splitk(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, ctypes.byref(e),
+                                  part.data_ptr(), part.numel() * 4, ksplit, L.stream_ptr()),
+            "vtd_gemm_splitk")
+    torch.cuda.synchronize()
+    ref64 = _np_act(act, (A.double() @ Bt.double().T + bias.double()).cpu().numpy())
+    if resid is not None:
+        ref64 = ref64 + resid.double().cpu().numpy()
+    got = out.double().cpu().numpy()
+    tol = 2e-5 if out_dtype == 0 else 8e-3
+    err = np.abs(got - ref64) / np.maximum(np.abs(ref64), 1.0)
+    assert err.max() < tol, err.max()
+    # the unsplit kernel on the same operands: equal up to fp32 summation order (f32 out)
+    # or one bf16 rounding step (bf16 out)
+    out1 = torch.full((M, N), float("nan"), device=cuda, dtype=odt)
+    _gemm(L, A, Bt, L.BF16, bias=bias, act=act, resid=resid, out=out1, out_dtype=out_dtype)
+    d = (out1.double() - out.double()).abs().cpu().numpy() / np.maximum(np.abs(ref64), 1.0)
+    assert d.max() < (1e-5 if out_dtype == 0 else 8e-3), d.max()
+
+
+def test_gemm_splitk_choice_and_args(L, cuda):
+    """The forward's split counts for the C2 head (B x 17 = 2176 rows per micro-batch) and
+    argument checks (ksplit < 2, short partial buffer, an empty split)."""
+    c = L.lib.vtd_gemm_splitk_choice
+    assert c(2176, 4352, 8704, L.BF16) == 2
+    assert c(2176, 2176, 4352, L.BF16) == 4
+    assert c(2176, 8704, 256, L.BF16) == 1          # short K
+    assert c(50176, 768, 768, L.BF16) == 1          # many tiles
+    assert c(2176, 4352, 8704, L.F32) == 1          # bf16 only
+    e = L.VtdEpilogue()
+    for ks, nbytes, K in ((1, 1 << 30, 512), (2, 16, 512), (9, 1 << 30, 512)):
+        with pytest.raises(ValueError):
+            L.check(L.lib.vtd_gemm_splitk(64, 64, K, 1, K, 1, K, ctypes.byref(e), 1, nbytes, ks,
+                                          L.stream_ptr()), "gemm_splitk")
+
+
+@pytest.mark.parametrize("M,N,K,act", [(6400, 2304, 768, 0), (6400, 3072, 768, 1),
+                                       (8192, 1024, 1024, 0), (6400, 776, 768, 1)])
+def test_gemm_ln_fused_finalize(L, cuda, monkeypatch, M, N, K, act):
+    """vtd_gemm_ln: the pp2 kernel merges each row's producer partials itself (full tiles,
+    12 / 16 slots) and leaves epi->lnstat untouched; VTD_LN_FINALIZE=1 (and any shape the
+    fused path does not serve: N = 776) runs vtd_layernorm_stats_finalize first.  Rows carry
+    distinct offsets (a wrong row's statistics would show), checked against fp64
+    LN -> Dense -> act, and the two paths against each other."""
+    g = torch.Generator(device=cuda).manual_seed(M + N + K + act)
+    x = (torch.randn(M, K, generator=g, device=cuda) * (1 + torch.rand(M, 1, generator=g, device=cuda) * 3)
+         + 6 * torch.randn(M, 1, generator=g, device=cuda)).to(torch.bfloat16)
+    w = torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)
+    gamma = 1 + 0.2 * torch.randn(K, generator=g, device=cuda)
+    beta = 0.3 * torch.randn(K, generator=g, device=cuda)
+    b = torch.randn(N, generator=g, device=cuda)
+    wo = torch.zeros(N, K, device=cuda).to(torch.bfloat16)
+    bo, cs = torch.zeros(N, device=cuda), torch.zeros(N, device=cuda)
+    L.check(L.lib.vtd_fold_layernorm(w.data_ptr(), N, K, K, gamma.data_ptr(), beta.data_ptr(),
+                                     b.data_ptr(), wo.data_ptr(), K, L.BF16, bo.data_ptr(),
+                                     cs.data_ptr(), L.stream_ptr()), "fold")
+    slots = K // 64
+    xb = x.float().view(M, slots, 64)                 # the producer's centred partials
+    bm = xb.mean(2)
+    part = torch.stack([bm, ((xb - bm[..., None]) ** 2).sum(2)], 2).contiguous()
+
+    def run(sep):
+        if sep:
+            monkeypatch.setenv("VTD_LN_FINALIZE", "1")
+        else:
+            monkeypatch.delenv("VTD_LN_FINALIZE", raising=False)
+        st = torch.full((M, 2), float("nan"), device=cuda)
+        out = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
+        e = L.VtdEpilogue()
+        e.bias, e.act, e.out, e.ldo, e.out_dtype = bo.data_ptr(), act, out.data_ptr(), N, L.BF16
+        e.lnstat, e.colsum = st.data_ptr(), cs.data_ptr()
+        L.check(L.lib.vtd_gemm_ln(M, N, K, x.data_ptr(), K, wo.data_ptr(), K, L.BF16,
+                                  ctypes.byref(e), part.data_ptr(), slots, K, 1e-3,
+                                  L.stream_ptr()), "gemm_ln")
+        torch.cuda.synchronize()
+        return out, st
+
+    fused, st_f = run(False)
+    sep, st_s = run(True)
+    assert torch.isfinite(st_s).all()
+    if N % 256 == 0:
+        assert torch.isnan(st_f).all()                # the fused path wrote no statistics
+    h = ref.layer_norm(x.double().cpu().numpy(), gamma.double().cpu().numpy(),
+                       beta.double().cpu().numpy())
+    ref64 = _np_act(act, h @ w.double().cpu().numpy().T + b.double().cpu().numpy())
+    for got in (fused, sep):
+        err = np.abs(got.double().cpu().numpy() - ref64) / np.maximum(np.abs(ref64), 1.0)
+        assert err.max() < 1.6e-2, err.max()
+    d = (fused.double() - sep.double()).abs() / sep.double().abs().clamp(min=1.0)
+    assert d.max().item() <= 2 ** -7, d.max().item()   # at most a bf16 rounding step apart

@@ -160,6 +160,38 @@ __device__ __forceinline__ float act_gelu(float x) {
   const float e = __builtin_amdgcn_exp2f(x * __builtin_fmaf(c1, x * x, c0));
   return x * __builtin_amdgcn_rcpf(1.f + e);
 }
+// LayerNorm row statistics from a producer GEMM's S centred partials per 64-column block
+// (block mean, sum of squared deviations), already in registers as S / 2 16-B words: Chan's
+// pairwise merge for equal counts relative to the first block mean (ln_stats_finalize_s_kernel
+// and the pp2 GEMM's fused finalize share this, so both give identical (mean, rstd)).
+template <int S>
+__device__ __forceinline__ float2 ln_merge_partials(const f32x4 (&v)[S / 2], int D, float eps) {
+  // no FMA contraction: the same instructions wherever this is inlined
+#pragma clang fp contract(off)
+  float2 t[S];
+#pragma unroll
+  for (int b = 0; b < S / 2; ++b) {
+    t[2 * b] = float2{v[b][0], v[b][1]};
+    t[2 * b + 1] = float2{v[b][2], v[b][3]};
+  }
+  const float m0 = t[0].x;
+  float ds = 0.f, q = 0.f;
+#pragma unroll
+  for (int b = 0; b < S; ++b) {
+    ds += t[b].x - m0;
+    q += t[b].y;
+  }
+  const float dmean = ds / S;
+  float between = 0.f;
+#pragma unroll
+  for (int b = 0; b < S; ++b) {
+    const float dv = (t[b].x - m0) - dmean;
+    between += dv * dv;
+  }
+  const float var = (q + 64.f * between) / D;
+  return float2{m0 + dmean, 1.f / sqrtf(var + eps)};
+}
+
 // Two values at once: the ordinary f32 arithmetic through the packed VALU
 // (v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32, one instruction per pair), the
 // transcendentals one by one (there is no packed v_exp_f32 / v_rcp_f32).  Same operations,

@@ -511,6 +511,24 @@ __global__ __launch_bounds__(256) void ln_stats_finalize_kernel(const float2* __
   stat[r] = float2{m0 + dmean, 1.f / sqrtf(var + eps)};
 }
 
+// The same with the slot count known at compile time: the row's S partials are loaded as
+// S / 2 16-B words before any arithmetic (one memory round trip instead of a dependent
+// chain); same operations in the same order as ln_stats_finalize_kernel (identical results).
+template <int S>
+__global__ __launch_bounds__(256) void ln_stats_finalize_s_kernel(const float4* __restrict__ part,
+                                                                  int64_t rows, int D, float eps,
+                                                                  float2* __restrict__ stat) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= rows) return;
+  f32x4 v[S / 2];
+#pragma unroll
+  for (int b = 0; b < S / 2; ++b) {
+    const float4 w = part[r * (S / 2) + b];
+    v[b] = f32x4{w.x, w.y, w.z, w.w};
+  }
+  stat[r] = ln_merge_partials<S>(v, D, eps);
+}
+
 // LayerNorm fold of one consumer Dense layer (one-time weight preparation): one wave per
 // output row n; fp64 sums (bias' from the fp32 W, colsum from the rounded stored W').
 template <typename TO>
@@ -757,6 +775,17 @@ int ln_stats_finalize_launch(const float* part, int64_t rows, int slots, int D, 
   VTD_CHECK_ARG(reinterpret_cast<uintptr_t>(part) % 8 == 0 && reinterpret_cast<uintptr_t>(stat) % 8 == 0,
                 "layernorm_stats_finalize: alignment");
   ProfScope ps(st, PROF_LN, 0.0);
+  // the common widths: every partial loaded at once (16-B loads), one memory round trip
+  if (slots == 12 || slots == 16) {
+    if (reinterpret_cast<uintptr_t>(part) % 16 == 0) {
+      auto k = slots == 12 ? ln_stats_finalize_s_kernel<12> : ln_stats_finalize_s_kernel<16>;
+      hipLaunchKernelGGL(k, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st,
+                         reinterpret_cast<const float4*>(part), rows, D, eps,
+                         reinterpret_cast<float2*>(stat));
+      VTD_LAUNCH_CHECK("layernorm_stats_finalize");
+      return VTD_OK;
+    }
+  }
   hipLaunchKernelGGL(ln_stats_finalize_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0,
                      st, reinterpret_cast<const float2*>(part), rows, slots, D, eps,
                      reinterpret_cast<float2*>(stat));

@@ -171,13 +171,17 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
   constexpr int ACT = EPI & 3;
   constexpr bool OUT_BF16 = (EPI & 4) != 0;
   constexpr bool RESID = (EPI & 8) != 0;
+  constexpr bool NOBIAS = (EPI & EPI_PARTIAL) != 0;   // split-K partial: raw fp32 sums
   constexpr int ES = 68;
   constexpr int NB = PR / 16;            // accumulator row blocks per pass
   constexpr int NIT = PR / 8;            // row-vector iterations per pass
   const int fr = lane & 15, fg = lane >> 4;
   const int c8 = (lane & 7) * 8, rsub = lane >> 3;
-  const f32x4 b0 = *reinterpret_cast<const f32x4*>(e.bias + n_base + c8);
-  const f32x4 b1 = *reinterpret_cast<const f32x4*>(e.bias + n_base + c8 + 4);
+  f32x4 b0 = {}, b1 = {};
+  if constexpr (!NOBIAS) {
+    b0 = *reinterpret_cast<const f32x4*>(e.bias + n_base + c8);
+    b1 = *reinterpret_cast<const f32x4*>(e.bias + n_base + c8 + 4);
+  }
   f32x4 cs0 = {}, cs1 = {};
   if (e.lnstat) {
     cs0 = *reinterpret_cast<const f32x4*>(e.colsum + n_base + c8);
@@ -441,9 +445,16 @@ __device__ __forceinline__ void pp2_issue(char* smem, const PP2BufSrc& src, int 
                                              kt * 128, 0, 0);
 }
 
-template <bool TR>
+struct NoOp {
+  __device__ void operator()() const {}
+};
+
+// after_prologue(): runs once K-tile 0 (and every older vector-memory load) has landed,
+// before the first barrier (the fused LayerNorm finalize merges its partials there)
+template <bool TR, class F = NoOp>
 __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, const PP2BufSrc& src,
-                                             int nk, int wave, int wm, int wn, int fr, int fg) {
+                                             int nk, int wave, int wm, int wn, int fr, int fg,
+                                             F&& after_prologue = NoOp{}) {
   // prologue: tile 0 complete, tile 1's X0/Y0/Y1 in flight
   pp2_issue<0>(smem, src, wave, 0, 0);
   pp2_issue<2>(smem, src, wave, 0, 0);
@@ -457,6 +468,7 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  after_prologue();
   pp_barrier();
   if (wm == 1) pp_barrier();                 // stagger G1 by one barrier
   const int ra = wm * 64, rb = wn * 32;      // group rows of this wave's quads
@@ -610,38 +622,76 @@ __device__ __forceinline__ void epilogue_direct_generic(const f32x4 (&acc)[8][4]
   }
 }
 
+// ksplit > 1 (split-K, EPI_PARTIAL or EPI_GENERIC without bias / activation): the grid holds
+// ksplit x tiles workgroups; workgroup v (after the XCD remap) takes split v / tiles of tile
+// v % tiles (neighbours on an XCD share a K range, so their panels are the same lines) and
+// writes its fp32 partial tile at e.out + split * e.split_stride; gemm_splitk_epilogue_kernel
+// sums the splits and applies the layer's epilogue.
 template <int EPI, bool TR = false>
 __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
     int M, int N, int K, const bf16_t* __restrict__ A, int lda,
-    const bf16_t* __restrict__ Bt, int ldb, int tiles_m, int tiles_n, EpiArgs e) {
+    const bf16_t* __restrict__ Bt, int ldb, int tiles_m, int tiles_n, EpiArgs e, int ksplit) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
-  const int nwg = tiles_m * tiles_n;
+  const int nt = tiles_m * tiles_n, nwg = nt * ksplit;
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int v = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int split = v / nt, tile = v - split * nt;
   int tm, tn;
   tile_coords(tile, tiles_m, tiles_n, e.ngw, tm, tn);
   const int m0 = tm * BBM, n0 = tn * BBN;
+  const int nk_all = K / 64, nks = (nk_all + ksplit - 1) / ksplit;
+  const int k0 = split * nks, nk = min(nks, nk_all - k0);   // host: every split non-empty
+  if (ksplit > 1) e.out = static_cast<float*>(e.out) + split * e.split_stride;
   PP2BufSrc src;
-  pp2b_sources<TR>(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane);
+  pp2b_sources<TR>(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane, k0 * 64);
   // LayerNorm-fold row statistics of the wave's 128 rows: issued before the K loop (the
   // oldest vector-memory op, so the loop's counted waits retire it), used in the epilogue
   float2 lst[2] = {float2{0.f, 0.f}, float2{0.f, 0.f}};
-  if (e.lnstat) {
-    lst[0] = e.lnstat[min(m0 + wm * 128 + lane, M - 1)];
-    lst[1] = e.lnstat[min(m0 + wm * 128 + 64 + lane, M - 1)];
+  // fused LayerNorm finalize (e.lnpart: the producer's 12 / 16 centred partials per row,
+  // full tiles on the fast epilogues only, see gemm_launch_ln): the rows' partials are
+  // loaded here, before the K loop's prologue DMA, and merged once it has landed
+  f32x4 pv[2][8];
+  const int lrow0 = min(m0 + wm * 128 + lane, M - 1), lrow1 = min(m0 + wm * 128 + 64 + lane, M - 1);
+  if (e.lnpart) {
+    const f32x4* p0 = reinterpret_cast<const f32x4*>(e.lnpart) + (int64_t)lrow0 * (e.lnslots / 2);
+    const f32x4* p1 = reinterpret_cast<const f32x4*>(e.lnpart) + (int64_t)lrow1 * (e.lnslots / 2);
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+      if (b < e.lnslots / 2) {
+        pv[0][b] = p0[b];
+        pv[1][b] = p1[b];
+      }
+  } else if (e.lnstat) {
+    lst[0] = e.lnstat[lrow0];
+    lst[1] = e.lnstat[lrow1];
   }
+  auto merge = [&] {
+    if (e.lnpart) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (e.lnslots == 12) {
+          f32x4 v[6];
+#pragma unroll
+          for (int b = 0; b < 6; ++b) v[b] = pv[h][b];
+          lst[h] = ln_merge_partials<12>(v, e.lnD, e.lneps);
+        } else {
+          lst[h] = ln_merge_partials<16>(pv[h], e.lnD, e.lneps);
+        }
+      }
+    }
+  };
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fg = lane >> 4;
-  pp2_mainloop<TR>(acc, smem, src, K / 64, wave, wm, wn, fr, fg);
+  pp2_mainloop<TR>(acc, smem, src, nk, wave, wm, wn, fr, fg, merge);
   const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
   if constexpr (TR) {
     if constexpr (EPI != EPI_GENERIC) {
@@ -930,18 +980,66 @@ int ln_stats_finalize_launch(const float* part, int64_t rows, int slots, int D, 
 
 template <int C>
 void pp2_launch(bool tr, dim3 g, hipStream_t stream, int M, int N, int K, const bf16_t* A, int lda,
-                const bf16_t* Bt, int ldb, int tiles_m, int tiles_n, const EpiArgs& e) {
+                const bf16_t* Bt, int ldb, int tiles_m, int tiles_n, const EpiArgs& e,
+                int ksplit = 1) {
   if (tr)
     hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, true>), g, dim3(BNT), 2 * BSTAGE, stream, M,
-                       N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
+                       N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e, ksplit);
   else
     hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, false>), g, dim3(BNT), 2 * BSTAGE, stream, M,
-                       N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
+                       N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e, ksplit);
+}
+
+void pp2_set_attributes() {
+  static std::once_flag once[kMaxDevices];
+  once_per_device(once, [] {
+#define VTD_PP_FN(C) reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, false>), \
+                     reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, true>),
+    const void* fns[] = {VTD_PP_FN(EPI_GENERIC) VTD_PP_FN(0) VTD_PP_FN(1) VTD_PP_FN(2)
+                         VTD_PP_FN(4) VTD_PP_FN(5) VTD_PP_FN(6) VTD_PP_FN(8) VTD_PP_FN(9)
+                         VTD_PP_FN(10) VTD_PP_FN(12) VTD_PP_FN(13) VTD_PP_FN(14)
+                         VTD_PP_FN(EPI_PARTIAL)};
+#undef VTD_PP_FN
+    for (const void* f : fns)
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
+  });
+}
+
+// Split-K reduction + the layer's epilogue: out[m][n..n+3] = epilogue(sum over the splits of
+// part[s][m][n..n+3]) through the shared row-vector epilogue (bias, activation, residual,
+// scatter, out2, fused decode; bounds), one thread per 4 columns.  The splits are summed in
+// split order (deterministic).
+__global__ __launch_bounds__(256) void gemm_splitk_epilogue_kernel(
+    const float* __restrict__ part, int ksplit, int64_t stride, int M, int N, int ldp,
+    EpiArgs e) {
+  const int nq = (N + 3) >> 2;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)M * nq) return;
+  const int m = (int)(i / nq), n = (int)(i - (int64_t)m * nq) * 4;
+  const float* p = part + (int64_t)m * ldp + n;
+  f32x4 v = *reinterpret_cast<const f32x4*>(p);
+  for (int s = 1; s < ksplit; ++s) v += *reinterpret_cast<const f32x4*>(p + s * stride);
+  epi_store4(e, M, N, m, n, v);
 }
 
 int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
                    int dtype, const vtd_epilogue* epi, hipStream_t stream, double flops,
                    const float* lnpart, int lnslots, int lnD, float lneps);
+
+// whether the pp2 kernel can take its fast (specialised) epilogues for this epilogue
+bool pp2_fast_epilogue(const vtd_epilogue* e) {
+  auto al16 = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
+  return e->bias && !e->detections && e->scatter_tokens <= 0 && e->ldo % 8 == 0 &&
+         (!e->resid || e->ldr % 8 == 0) && al16(e->out) && al16(e->bias) &&
+         (!e->resid || al16(e->resid)) && (!e->out2 || (e->ldo2 % 8 == 0 && al16(e->out2)));
+}
+
+// VTD_LN_FINALIZE=1: always launch the separate LayerNorm finalize (A/B switch, read per
+// call: 24 getenv per C2 forward)
+bool ln_fuse_enabled() {
+  const char* v = getenv("VTD_LN_FINALIZE");
+  return !(v && atoi(v) != 0);
+}
 
 int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
                 int dtype, const vtd_epilogue* epi, hipStream_t stream, double flops) {
@@ -974,7 +1072,15 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
   if (epi->statout && !gemm_emits_stats(M, N, dtype, epi))
     return fail(VTD_ERR_UNSUPPORTED, "gemm: statout needs full 256 x 256 tiles on the bf16 "
                                      "fast epilogues (see gemm_emits_stats)");
-  if (lnpart) {
+  // fused finalize: the pp2 kernel merges the partials itself (full tiles on the fast
+  // epilogues, which take the rows' statistics from the merged registers); every other
+  // path reads epi->lnstat, written by ln_stats_finalize first
+  const bool fuse_ln =
+      lnpart && epi->lnstat && dtype == VTD_BF16 && gemm_variant() == 10 && ln_fuse_enabled() &&
+      ((M + BBM - 1) / BBM) * ((N + BBN - 1) / BBN) >= kMinBigTiles && N > 64 &&
+      M % BBM == 0 && N % BBN == 0 && (lnslots == 12 || lnslots == 16) && lnD == 64 * lnslots &&
+      reinterpret_cast<uintptr_t>(lnpart) % 16 == 0 && pp2_fast_epilogue(epi);
+  if (lnpart && !fuse_ln) {
     const int rc = ln_stats_finalize_launch(lnpart, M, lnslots, lnD, lneps,
                                             const_cast<float*>(epi->lnstat), stream);
     if (rc) return rc;
@@ -992,23 +1098,14 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
       VTD_LAUNCH_CHECK("gemm");
       return VTD_OK;
     }
-    static std::once_flag once[kMaxDevices];
-    once_per_device(once, [] {
-#define VTD_PP_FN(C) reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, false>), \
-                     reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, true>),
-      const void* fns[] = {VTD_PP_FN(EPI_GENERIC) VTD_PP_FN(0) VTD_PP_FN(1) VTD_PP_FN(2)
-                           VTD_PP_FN(4) VTD_PP_FN(5) VTD_PP_FN(6) VTD_PP_FN(8) VTD_PP_FN(9)
-                           VTD_PP_FN(10) VTD_PP_FN(12) VTD_PP_FN(13) VTD_PP_FN(14)};
-#undef VTD_PP_FN
-      for (const void* f : fns)
-        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
-    });
+    pp2_set_attributes();
     EpiArgs e = make_epi_args(epi);
     e.ngw = ngw;
-    auto al16 = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
-    const bool fast = e.bias && !e.dets && e.scatter_tokens <= 0 && e.ldo % 8 == 0 &&
-                      (!e.resid || e.ldr % 8 == 0) && al16(e.out) && al16(e.bias) &&
-                      (!e.resid || al16(e.resid)) && (!e.out2 || (e.ldo2 % 8 == 0 && al16(e.out2)));
+    if (fuse_ln) {
+      e.lnpart = reinterpret_cast<const float2*>(lnpart);
+      e.lnslots = lnslots; e.lnD = lnD; e.lneps = lneps;
+    }
+    const bool fast = pp2_fast_epilogue(epi);
     const int code = fast ? epi_code(e.act, e.out_dtype == VTD_BF16, e.resid != nullptr)
                           : EPI_GENERIC;
     // transposed accumulators + register-direct epilogue for activation layers (mlp1 -5 %,
@@ -1037,6 +1134,67 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
                          static_cast<const float*>(A), lda, static_cast<const float*>(Bt), ldb, e);
   }
   VTD_LAUNCH_CHECK("gemm");
+  return VTD_OK;
+}
+
+// Split-K for few-tile, long-K bf16 problems (the detection head's Dense layers at
+// B x 17 rows): the number of K splits that brings the 256 x 256-tile grid near one full
+// round of the chip (kSplitTarget workgroups), every split keeping >= kSplitMinSteps K-steps
+// so its operand traffic stays well above its 256 KiB fp32 partial tile; 1 = no split.
+// Fixed targets (not the device's CU count) so that workspace sizing needs no device.
+// VTD_SPLITK=0 disables it (A/B switch, read per call).
+constexpr int kSplitTarget = 256, kSplitMinSteps = 8;
+int gemm_splitk_choice(int M, int N, int K, int dtype) {
+  const char* v = getenv("VTD_SPLITK");
+  if (v && atoi(v) == 0) return 1;
+  if (dtype != VTD_BF16 || N <= 64 || K % 64 != 0 || M <= 0) return 1;
+  const int tiles = ((M + BBM - 1) / BBM) * ((N + BBN - 1) / BBN);
+  const int nk = K / 64;
+  if (tiles >= (3 * kSplitTarget) / 4) return 1;
+  const int s = std::min((kSplitTarget + tiles - 1) / tiles, nk / kSplitMinSteps);
+  if (s < 2) return 1;
+  const int nks = (nk + s - 1) / s;
+  return (nk + nks - 1) / nks;               // every split non-empty
+}
+
+// C = epilogue(A Bt^T) as ksplit pp2 K-ranges writing fp32 partial tiles into part
+// ([ksplit][M][N] floats), then gemm_splitk_epilogue_kernel.  Same products as the unsplit
+// kernels, summed in a different order (fp32).
+int gemm_splitk_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
+                       const vtd_epilogue* epi, float* part, int ksplit, hipStream_t stream,
+                       double flops) {
+  VTD_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 64 == 0 && N % 4 == 0,
+                "gemm_splitk: M, N, K positive, K % 64, N % 4");
+  VTD_CHECK_ARG(A && Bt && epi && epi->out && part, "gemm_splitk: null pointer");
+  VTD_CHECK_ARG(lda >= K && ldb >= K && lda % 8 == 0 && ldb % 8 == 0,
+                "gemm_splitk: lda/ldb must be >= K and multiples of 8");
+  VTD_CHECK_ARG(ksplit >= 2 && ksplit <= K / 64, "gemm_splitk: ksplit");
+  VTD_CHECK_ARG(!epi->statout && !epi->lnstat,
+                "gemm_splitk: LayerNorm statistics / fold are not supported");
+  const int nk = K / 64, nks = (nk + ksplit - 1) / ksplit;
+  VTD_CHECK_ARG((ksplit - 1) * nks < nk, "gemm_splitk: an empty split");
+  ProfScope ps(stream, PROF_GEMM, flops > 0 ? flops : 2.0 * M * N * (double)K);
+  pp2_set_attributes();
+  const int tiles_m = (M + BBM - 1) / BBM, tiles_n = (N + BBN - 1) / BBN;
+  EpiArgs pe{};
+  pe.out = part; pe.ldo = N; pe.out_dtype = VTD_F32;
+  pe.ngw = tile_group_width(tiles_n);
+  pe.split_stride = (int64_t)M * N;
+  const bf16_t* a16 = static_cast<const bf16_t*>(A);
+  const bf16_t* b16 = static_cast<const bf16_t*>(Bt);
+  const dim3 g(tiles_m * tiles_n * ksplit);
+  if (N % 8 == 0 && reinterpret_cast<uintptr_t>(part) % 16 == 0)
+    pp2_launch<EPI_PARTIAL>(false, g, stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, pe,
+                            ksplit);
+  else
+    pp2_launch<EPI_GENERIC>(false, g, stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, pe,
+                            ksplit);
+  VTD_LAUNCH_CHECK("gemm_splitk");
+  const EpiArgs e = make_epi_args(epi);
+  const int64_t work = (int64_t)M * ((N + 3) / 4);
+  hipLaunchKernelGGL(gemm_splitk_epilogue_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256),
+                     0, stream, part, ksplit, (int64_t)M * N, M, N, N, e);
+  VTD_LAUNCH_CHECK("gemm_splitk_epilogue");
   return VTD_OK;
 }
 
@@ -1126,4 +1284,27 @@ extern "C" int vtd_gemm_mx8(int M, int N, int K, const uint8_t* A_dev, int lda,
                             const vtd_epilogue* epi, void* stream) {
   return vtd::gemm_mx8_launch(M, N, K, A_dev, lda, sA_dev, sa_rows, Bt_dev, ldb, sB_dev, sb_rows,
                               epi, static_cast<hipStream_t>(stream), 0.0);
+}
+
+extern "C" int vtd_gemm_splitk(int M, int N, int K, const void* A_dev, int lda,
+                               const void* Bt_dev, int ldb, const vtd_epilogue* epi,
+                               float* part_dev, size_t part_bytes, int ksplit, void* stream) {
+  if (ksplit < 2 || part_bytes < (size_t)ksplit * (size_t)std::max(M, 0) * std::max(N, 0) * 4)
+    return vtd::fail(VTD_ERR_INVALID_ARG, "gemm_splitk: ksplit < 2 or part_bytes too small");
+  return vtd::gemm_splitk_launch(M, N, K, A_dev, lda, Bt_dev, ldb, epi, part_dev, ksplit,
+                                 static_cast<hipStream_t>(stream), 0.0);
+}
+
+extern "C" int vtd_gemm_splitk_choice(int M, int N, int K, int dtype) {
+  return vtd::gemm_splitk_choice(M, N, K, dtype);
+}
+
+extern "C" int vtd_gemm_ln(int M, int N, int K, const void* A_dev, int lda, const void* Bt_dev,
+                           int ldb, int dtype, const vtd_epilogue* epi, const float* lnpart_dev,
+                           int lnslots, int lnD, float lneps, void* stream) {
+  if (!lnpart_dev || !epi || !epi->lnstat || !epi->colsum)
+    return vtd::fail(VTD_ERR_INVALID_ARG, "gemm_ln: lnpart, epi->lnstat and epi->colsum are required");
+  return vtd::gemm_launch_ln(M, N, K, A_dev, lda, Bt_dev, ldb, dtype, epi,
+                             static_cast<hipStream_t>(stream), 0.0, lnpart_dev, lnslots, lnD,
+                             lneps);
 }

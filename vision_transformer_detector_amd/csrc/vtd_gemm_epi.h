@@ -34,6 +34,9 @@ struct EpiArgs {
   // tile order (pp2): 0 = row-major (an XCD walks all n-tiles of consecutive m-rows); g > 0 =
   // n-groups of g tiles, m-rows inside a group (an XCD keeps a group's weight panels in L2)
   int ngw;
+  // split-K partial launches (pp2, ksplit > 1): split s writes its fp32 partial tile at
+  // out + s * split_stride (elements)
+  int64_t split_stride;
 };
 
 // bf16 output row vector store of the fast epilogues; build-time A/B knob VTD_OUT_NT: 1 =
@@ -216,6 +219,8 @@ __device__ __forceinline__ void epi_store4(const EpiArgs& e, int M, int N, int m
 
 // ---- specialized epilogue (EPI = act | out_bf16 << 2 | resid << 3), full tiles only
 constexpr int EPI_GENERIC = -1;
+// pp2 split-K partial launches: fp32 raw sums, no bias / activation / residual (vtd_gemm.hip)
+constexpr int EPI_PARTIAL = 16;
 __host__ __device__ constexpr int epi_code(int act, bool out_bf16, bool resid) {
   return act | (out_bf16 ? 4 : 0) | (resid ? 8 : 0);
 }

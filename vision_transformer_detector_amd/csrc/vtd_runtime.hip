@@ -1,6 +1,7 @@
 // Host runtime of libvtd.so: error state, graph shapes, workspace plan, the whole
 // forward (`model(images, training=False)`, vtd.py:498-583) as one sequence of
 // launches on the caller's stream, and optional hipEvent per-launch profiling.
+#include <atomic>
 #include <algorithm>
 #include <cmath>
 #include <mutex>
@@ -25,6 +26,10 @@ int ln_stats_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx, fl
 int ln_stats_finalize_launch(const float* part, int64_t rows, int slots, int D, float eps,
                              float* stat, hipStream_t st);
 bool gemm_emits_stats(int M, int N, int dtype, const vtd_epilogue* e);
+int gemm_splitk_choice(int M, int N, int K, int dtype);
+int gemm_splitk_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
+                       const vtd_epilogue* epi, float* part, int ksplit, hipStream_t stream,
+                       double flops);
 int patches_launch(const float* img, int B, int H, int W, int C, int p, void* out, int ldo,
                    int dtype, hipStream_t st);
 int attention_mx8_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqkv,
@@ -172,7 +177,7 @@ static int derive(const vtd_config* c, vtd_dims* d) {
 namespace {
 struct Plan {
   size_t patches, x, xb, h, stat, pstat, qkv, attn, mlp0, mlp1, u, head0, head1, q8, s8, q8b, s8b,
-      total;
+      splitk, total;
   int k8_max;                       // widest MX-fp8 GEMM K (VTD_FP8)
   int64_t s8_rows;                  // activation scale rows (rows rounded up to 4)
 };
@@ -216,6 +221,13 @@ Plan make_plan(const vtd_config* c, const vtd_dims& d) {
   p.u = take(HR * d.tokens_p * es);
   p.head0 = take(HR * head_max * es);
   p.head1 = take(HR * head_max * es);
+  // fp32 split-K partials of the head's few-tile, long-K Dense layers (gemm_splitk_choice)
+  size_t sk = 0;
+  for (int j = 0, k = d.tokens_p; j < d.n_head; k = d.head_units_p[j], ++j) {
+    const int s = gemm_splitk_choice((int)HR, d.head_units_p[j], k, act_dtype(c->dtype));
+    if (s > 1) sk = std::max(sk, (size_t)s * HR * d.head_units_p[j] * 4);
+  }
+  p.splitk = take(sk);
   // VTD_FP8: one MX-fp8 copy of the current encoder GEMM's A operand + its scales
   p.k8_max = 0;
   p.s8_rows = round_up((int64_t)R, 4);
@@ -449,12 +461,21 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   // VTD_DIAG builds only (timing diagnostics, WRONG outputs): VTD_DIAG_NOFIN skips the
   // LayerNorm finalize launches, VTD_DIAG_NOATTN the attention launches, VTD_DIAG_NOHEAD
   // the detection head
-  static const bool diag_nofin = VTD_DIAG && getenv("VTD_DIAG_NOFIN");
+  // (VTD_DIAG_NOFIN=n: after the first n finalize launches, so the consumers keep applying
+  // the last real row statistics: activations stay realistic, MFMA power and clock with them)
+  static const int diag_nofin = VTD_DIAG && getenv("VTD_DIAG_NOFIN") ? atoi(getenv("VTD_DIAG_NOFIN")) : -1;
+  static std::atomic<int> diag_fin_count{0};
   static const bool diag_noattn = VTD_DIAG && getenv("VTD_DIAG_NOATTN");
+  // producer partials the next folded GEMM finalizes (gemm_launch_ln: inside the pp2 kernel
+  // where it can, else by ln_stats_finalize before it)
+  const float* fin_part = nullptr;
   auto row_stats = [&]() -> int {
-    if (diag_nofin) return VTD_OK;
-    return partials ? ln_stats_finalize_launch(pstat, R, nslot, D, 1e-3f, stat, st)
-                    : ln_stats_launch(x, rdt, R, D, Dp, 1e-3f, stat, st);
+    if (diag_nofin >= 0 && partials && diag_fin_count.fetch_add(1) >= diag_nofin) return VTD_OK;
+    if (partials) {
+      fin_part = pstat;
+      return VTD_OK;
+    }
+    return ln_stats_launch(x, rdt, R, D, Dp, 1e-3f, stat, st);
   };
   void* xb = ws + P.xb;
   void* h = ws + P.h;
@@ -472,7 +493,11 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   // against the MX-fp8 weights (W [Np][K8], S [K8/128][Np][4])
   auto enc_gemm = [&](int Np, int K, const void* a, const void* W, const uint8_t* S,
                       const vtd_epilogue* e, double flops) -> int {
-    if (!fp8) return gemm_launch(M, Np, K, a, K, W, K, dt, e, st, flops);
+    if (!fp8) {
+      const float* lp = fin_part;
+      fin_part = nullptr;
+      return gemm_launch_ln(M, Np, K, a, K, W, K, dt, e, st, flops, lp, nslot, D, 1e-3f);
+    }
     const int K8 = k8_of(K);
     int r = quantize_mx8_launch(a, VTD_BF16, R, K, K, K8, q8, K8, s8, P.s8_rows, st);
     if (r) return r;
@@ -642,8 +667,11 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     vtd_epilogue e{};
     e.bias = w->b_head[j]; e.act = act;
     e.out = head[j & 1]; e.ldo = d.head_units_p[j]; e.out_dtype = dt;
-    rc = gemm_launch(HR, d.head_units_p[j], k, a, k, w->w_head[j], k, dt, &e, st,
-                     2.0 * HR * (double)kv * d.head_units[j]);
+    const double fl = 2.0 * HR * (double)kv * d.head_units[j];
+    const int ks = gemm_splitk_choice(HR, d.head_units_p[j], k, dt);
+    rc = ks > 1 ? gemm_splitk_launch(HR, d.head_units_p[j], k, a, k, w->w_head[j], k, &e,
+                                     reinterpret_cast<float*>(ws + P.splitk), ks, st, fl)
+                : gemm_launch(HR, d.head_units_p[j], k, a, k, w->w_head[j], k, dt, &e, st, fl);
     if (rc) return rc;
     a = head[j & 1];
     k = d.head_units_p[j];
