@@ -206,17 +206,6 @@ int vtd_gemm_splitk(int M, int N, int K, const void* A_dev, int lda, const void*
                     int ldb, const vtd_epilogue* epi, float* part_dev, size_t part_bytes,
                     int ksplit, void* stream);
 int vtd_gemm_splitk_choice(int M, int N, int K, int dtype);
-/* vtd_gemm for a folded LayerNorm whose row statistics are still a producer's centred
- * partials (`statout` layout: lnslots (block mean, M2) pairs per row, D = 64 * lnslots,
- * eps): what vtd_forward runs for the query/key/value and first-MLP GEMMs.  Where the
- * 256-tile bf16 kernel serves every tile on its fast epilogues (M % 256 == N % 256 == 0,
- * lnslots 12 or 16, lnpart 16-B aligned) it merges each row's partials itself (Chan, the
- * arithmetic of vtd_layernorm_stats_finalize) and epi->lnstat is not written; otherwise
- * vtd_layernorm_stats_finalize writes epi->lnstat first.  VTD_LN_FINALIZE=1 forces the
- * latter (read per call). */
-int vtd_gemm_ln(int M, int N, int K, const void* A_dev, int lda, const void* Bt_dev, int ldb,
-                int dtype, const vtd_epilogue* epi, const float* lnpart_dev, int lnslots,
-                int lnD, float lneps, void* stream);
 
 /* MX-fp8 operands (OCP MX: e4m3 elements, one E8M0 scale byte e = 2^(e-127) per 32
  * consecutive K elements).  vtd_quantize_mx8: x [rows][ldx] (x_dtype F32 or BF16), first

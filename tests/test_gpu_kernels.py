@@ -684,59 +684,3 @@ def test_gemm_splitk_choice_and_args(L, cuda):
         with pytest.raises(ValueError):
             L.check(L.lib.vtd_gemm_splitk(64, 64, K, 1, K, 1, K, ctypes.byref(e), 1, nbytes, ks,
                                           L.stream_ptr()), "gemm_splitk")
-
-
-@pytest.mark.parametrize("M,N,K,act", [(6400, 2304, 768, 0), (6400, 3072, 768, 1),
-                                       (8192, 1024, 1024, 0), (6400, 776, 768, 1)])
-def test_gemm_ln_fused_finalize(L, cuda, monkeypatch, M, N, K, act):
-    """vtd_gemm_ln: the pp2 kernel merges each row's producer partials itself (full tiles,
-    12 / 16 slots) and leaves epi->lnstat untouched; VTD_LN_FINALIZE=1 (and any shape the
-    fused path does not serve: N = 776) runs vtd_layernorm_stats_finalize first.  Rows carry
-    distinct offsets (a wrong row's statistics would show), checked against fp64
-    LN -> Dense -> act, and the two paths against each other."""
-    g = torch.Generator(device=cuda).manual_seed(M + N + K + act)
-    x = (torch.randn(M, K, generator=g, device=cuda) * (1 + torch.rand(M, 1, generator=g, device=cuda) * 3)
-         + 6 * torch.randn(M, 1, generator=g, device=cuda)).to(torch.bfloat16)
-    w = torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)
-    gamma = 1 + 0.2 * torch.randn(K, generator=g, device=cuda)
-    beta = 0.3 * torch.randn(K, generator=g, device=cuda)
-    b = torch.randn(N, generator=g, device=cuda)
-    wo = torch.zeros(N, K, device=cuda).to(torch.bfloat16)
-    bo, cs = torch.zeros(N, device=cuda), torch.zeros(N, device=cuda)
-    L.check(L.lib.vtd_fold_layernorm(w.data_ptr(), N, K, K, gamma.data_ptr(), beta.data_ptr(),
-                                     b.data_ptr(), wo.data_ptr(), K, L.BF16, bo.data_ptr(),
-                                     cs.data_ptr(), L.stream_ptr()), "fold")
-    slots = K // 64
-    xb = x.float().view(M, slots, 64)                 # the producer's centred partials
-    bm = xb.mean(2)
-    part = torch.stack([bm, ((xb - bm[..., None]) ** 2).sum(2)], 2).contiguous()
-
-    def run(sep):
-        if sep:
-            monkeypatch.setenv("VTD_LN_FINALIZE", "1")
-        else:
-            monkeypatch.delenv("VTD_LN_FINALIZE", raising=False)
-        st = torch.full((M, 2), float("nan"), device=cuda)
-        out = torch.full((M, N), float("nan"), device=cuda, dtype=torch.bfloat16)
-        e = L.VtdEpilogue()
-        e.bias, e.act, e.out, e.ldo, e.out_dtype = bo.data_ptr(), act, out.data_ptr(), N, L.BF16
-        e.lnstat, e.colsum = st.data_ptr(), cs.data_ptr()
-        L.check(L.lib.vtd_gemm_ln(M, N, K, x.data_ptr(), K, wo.data_ptr(), K, L.BF16,
-                                  ctypes.byref(e), part.data_ptr(), slots, K, 1e-3,
-                                  L.stream_ptr()), "gemm_ln")
-        torch.cuda.synchronize()
-        return out, st
-
-    fused, st_f = run(False)
-    sep, st_s = run(True)
-    assert torch.isfinite(st_s).all()
-    if N % 256 == 0:
-        assert torch.isnan(st_f).all()                # the fused path wrote no statistics
-    h = ref.layer_norm(x.double().cpu().numpy(), gamma.double().cpu().numpy(),
-                       beta.double().cpu().numpy())
-    ref64 = _np_act(act, h @ w.double().cpu().numpy().T + b.double().cpu().numpy())
-    for got in (fused, sep):
-        err = np.abs(got.double().cpu().numpy() - ref64) / np.maximum(np.abs(ref64), 1.0)
-        assert err.max() < 1.6e-2, err.max()
-    d = (fused.double() - sep.double()).abs() / sep.double().abs().clamp(min=1.0)
-    assert d.max().item() <= 2 ** -7, d.max().item()   # at most a bf16 rounding step apart

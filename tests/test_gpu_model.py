@@ -321,24 +321,3 @@ def test_removed_diagnostic_switches_do_not_change_logits(vtd, cuda, monkeypatch
             assert torch.equal(big(x), ref_big), (var, val)
             assert torch.equal(tiny(tx), ref_tiny), (var, val)
         monkeypatch.delenv(var)
-
-
-def test_fused_layernorm_finalize_equals_separate_launch(vtd, cuda, monkeypatch):
-    """The folded query/key/value and first-MLP GEMMs merge the producer's LayerNorm partials
-    themselves (pp2, full tiles: C2 at 128 images = two halves of 49 row tiles); with
-    VTD_LN_FINALIZE=1 ln_stats_finalize writes the statistics first.  Both run
-    ln_merge_partials on the same partials: the logits are the same bits."""
-    spec = json.load(open(os.path.join(GOLD, "seeded_forward.json")))["c2_vitb16_b1"]
-    kw = dict(spec["kwargs"])
-    w = V.init_weights(seed=spec["weight_seed"], perturb=spec["perturb"], **kw)
-    shape = V.resolve_kwargs(**kw)["input_shape"]
-    x = torch.from_numpy(V.synthetic_images(128, shape, seed=5)).to(cuda)
-    model = vtd.create_vision_transformer_detector(**kw, dtype="bfloat16")
-    model.set_weights(w)
-    monkeypatch.delenv("VTD_LN_FINALIZE", raising=False)
-    fused = model(x).clone()
-    monkeypatch.setenv("VTD_LN_FINALIZE", "1")
-    sep = model(x).clone()
-    assert torch.isfinite(fused).all()
-    d = (fused - sep).abs().max().item()
-    assert torch.equal(fused, sep), d

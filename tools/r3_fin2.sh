@@ -18,4 +18,7 @@ for r in 1 2; do
   run fused VTD_X=0
   run finlaunch VTD_LN_FINALIZE=1
   run nofin240 VTD_LIB_PATH=$D VTD_DIAG_NOFIN=240 VTD_LN_FINALIZE=1
+  run attngrid512 VTD_ATTN_GRID=512
+  run attngrid768 VTD_ATTN_GRID=768
+  run attngrid1536 VTD_ATTN_GRID=1536
 done

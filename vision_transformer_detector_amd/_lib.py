@@ -95,8 +95,6 @@ SIGNATURES = {
     "vtd_gemm_splitk": (c_int, [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int,
                                 ctypes.POINTER(VtdEpilogue), c_void_p, c_size_t, c_int, c_void_p]),
     "vtd_gemm_splitk_choice": (c_int, [c_int, c_int, c_int, c_int]),
-    "vtd_gemm_ln": (c_int, [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int,
-                            ctypes.POINTER(VtdEpilogue), c_void_p, c_int, c_int, c_float, c_void_p]),
     "vtd_quantize_mx8": (c_int, [c_void_p, c_int, c_int64, c_int, c_int, c_int, c_void_p, c_int,
                                  c_void_p, c_int64, c_void_p]),
     "vtd_layernorm_mx8": (c_int, [c_void_p, c_int, c_int64, c_int, c_int, c_void_p, c_void_p,

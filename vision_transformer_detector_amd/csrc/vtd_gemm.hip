@@ -445,16 +445,9 @@ __device__ __forceinline__ void pp2_issue(char* smem, const PP2BufSrc& src, int 
                                              kt * 128, 0, 0);
 }
 
-struct NoOp {
-  __device__ void operator()() const {}
-};
-
-// after_prologue(): runs once K-tile 0 (and every older vector-memory load) has landed,
-// before the first barrier (the fused LayerNorm finalize merges its partials there)
-template <bool TR, class F = NoOp>
+template <bool TR>
 __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, const PP2BufSrc& src,
-                                             int nk, int wave, int wm, int wn, int fr, int fg,
-                                             F&& after_prologue = NoOp{}) {
+                                             int nk, int wave, int wm, int wn, int fr, int fg) {
   // prologue: tile 0 complete, tile 1's X0/Y0/Y1 in flight
   pp2_issue<0>(smem, src, wave, 0, 0);
   pp2_issue<2>(smem, src, wave, 0, 0);
@@ -468,7 +461,6 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  after_prologue();
   pp_barrier();
   if (wm == 1) pp_barrier();                 // stagger G1 by one barrier
   const int ra = wm * 64, rb = wn * 32;      // group rows of this wave's quads
@@ -652,46 +644,17 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
   // LayerNorm-fold row statistics of the wave's 128 rows: issued before the K loop (the
   // oldest vector-memory op, so the loop's counted waits retire it), used in the epilogue
   float2 lst[2] = {float2{0.f, 0.f}, float2{0.f, 0.f}};
-  // fused LayerNorm finalize (e.lnpart: the producer's 12 / 16 centred partials per row,
-  // full tiles on the fast epilogues only, see gemm_launch_ln): the rows' partials are
-  // loaded here, before the K loop's prologue DMA, and merged once it has landed
-  f32x4 pv[2][8];
-  const int lrow0 = min(m0 + wm * 128 + lane, M - 1), lrow1 = min(m0 + wm * 128 + 64 + lane, M - 1);
-  if (e.lnpart) {
-    const f32x4* p0 = reinterpret_cast<const f32x4*>(e.lnpart) + (int64_t)lrow0 * (e.lnslots / 2);
-    const f32x4* p1 = reinterpret_cast<const f32x4*>(e.lnpart) + (int64_t)lrow1 * (e.lnslots / 2);
-#pragma unroll
-    for (int b = 0; b < 8; ++b)
-      if (b < e.lnslots / 2) {
-        pv[0][b] = p0[b];
-        pv[1][b] = p1[b];
-      }
-  } else if (e.lnstat) {
-    lst[0] = e.lnstat[lrow0];
-    lst[1] = e.lnstat[lrow1];
+  if (e.lnstat) {
+    lst[0] = e.lnstat[min(m0 + wm * 128 + lane, M - 1)];
+    lst[1] = e.lnstat[min(m0 + wm * 128 + 64 + lane, M - 1)];
   }
-  auto merge = [&] {
-    if (e.lnpart) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (e.lnslots == 12) {
-          f32x4 v[6];
-#pragma unroll
-          for (int b = 0; b < 6; ++b) v[b] = pv[h][b];
-          lst[h] = ln_merge_partials<12>(v, e.lnD, e.lneps);
-        } else {
-          lst[h] = ln_merge_partials<16>(pv[h], e.lnD, e.lneps);
-        }
-      }
-    }
-  };
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fg = lane >> 4;
-  pp2_mainloop<TR>(acc, smem, src, nk, wave, wm, wn, fr, fg, merge);
+  pp2_mainloop<TR>(acc, smem, src, nk, wave, wm, wn, fr, fg);
   const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
   if constexpr (TR) {
     if constexpr (EPI != EPI_GENERIC) {
@@ -1034,13 +997,6 @@ bool pp2_fast_epilogue(const vtd_epilogue* e) {
          (!e->resid || al16(e->resid)) && (!e->out2 || (e->ldo2 % 8 == 0 && al16(e->out2)));
 }
 
-// VTD_LN_FINALIZE=1: always launch the separate LayerNorm finalize (A/B switch, read per
-// call: 24 getenv per C2 forward)
-bool ln_fuse_enabled() {
-  const char* v = getenv("VTD_LN_FINALIZE");
-  return !(v && atoi(v) != 0);
-}
-
 int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
                 int dtype, const vtd_epilogue* epi, hipStream_t stream, double flops) {
   return gemm_launch_ln(M, N, K, A, lda, Bt, ldb, dtype, epi, stream, flops, nullptr, 0, 0, 0.f);
@@ -1072,15 +1028,7 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
   if (epi->statout && !gemm_emits_stats(M, N, dtype, epi))
     return fail(VTD_ERR_UNSUPPORTED, "gemm: statout needs full 256 x 256 tiles on the bf16 "
                                      "fast epilogues (see gemm_emits_stats)");
-  // fused finalize: the pp2 kernel merges the partials itself (full tiles on the fast
-  // epilogues, which take the rows' statistics from the merged registers); every other
-  // path reads epi->lnstat, written by ln_stats_finalize first
-  const bool fuse_ln =
-      lnpart && epi->lnstat && dtype == VTD_BF16 && gemm_variant() == 10 && ln_fuse_enabled() &&
-      ((M + BBM - 1) / BBM) * ((N + BBN - 1) / BBN) >= kMinBigTiles && N > 64 &&
-      M % BBM == 0 && N % BBN == 0 && (lnslots == 12 || lnslots == 16) && lnD == 64 * lnslots &&
-      reinterpret_cast<uintptr_t>(lnpart) % 16 == 0 && pp2_fast_epilogue(epi);
-  if (lnpart && !fuse_ln) {
+  if (lnpart) {
     const int rc = ln_stats_finalize_launch(lnpart, M, lnslots, lnD, lneps,
                                             const_cast<float*>(epi->lnstat), stream);
     if (rc) return rc;
@@ -1101,10 +1049,6 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
     pp2_set_attributes();
     EpiArgs e = make_epi_args(epi);
     e.ngw = ngw;
-    if (fuse_ln) {
-      e.lnpart = reinterpret_cast<const float2*>(lnpart);
-      e.lnslots = lnslots; e.lnD = lnD; e.lneps = lneps;
-    }
     const bool fast = pp2_fast_epilogue(epi);
     const int code = fast ? epi_code(e.act, e.out_dtype == VTD_BF16, e.resid != nullptr)
                           : EPI_GENERIC;
@@ -1297,14 +1241,4 @@ extern "C" int vtd_gemm_splitk(int M, int N, int K, const void* A_dev, int lda,
 
 extern "C" int vtd_gemm_splitk_choice(int M, int N, int K, int dtype) {
   return vtd::gemm_splitk_choice(M, N, K, dtype);
-}
-
-extern "C" int vtd_gemm_ln(int M, int N, int K, const void* A_dev, int lda, const void* Bt_dev,
-                           int ldb, int dtype, const vtd_epilogue* epi, const float* lnpart_dev,
-                           int lnslots, int lnD, float lneps, void* stream) {
-  if (!lnpart_dev || !epi || !epi->lnstat || !epi->colsum)
-    return vtd::fail(VTD_ERR_INVALID_ARG, "gemm_ln: lnpart, epi->lnstat and epi->colsum are required");
-  return vtd::gemm_launch_ln(M, N, K, A_dev, lda, Bt_dev, ldb, dtype, epi,
-                             static_cast<hipStream_t>(stream), 0.0, lnpart_dev, lnslots, lnD,
-                             lneps);
 }

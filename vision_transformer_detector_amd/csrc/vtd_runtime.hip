@@ -466,16 +466,10 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   static const int diag_nofin = VTD_DIAG && getenv("VTD_DIAG_NOFIN") ? atoi(getenv("VTD_DIAG_NOFIN")) : -1;
   static std::atomic<int> diag_fin_count{0};
   static const bool diag_noattn = VTD_DIAG && getenv("VTD_DIAG_NOATTN");
-  // producer partials the next folded GEMM finalizes (gemm_launch_ln: inside the pp2 kernel
-  // where it can, else by ln_stats_finalize before it)
-  const float* fin_part = nullptr;
   auto row_stats = [&]() -> int {
     if (diag_nofin >= 0 && partials && diag_fin_count.fetch_add(1) >= diag_nofin) return VTD_OK;
-    if (partials) {
-      fin_part = pstat;
-      return VTD_OK;
-    }
-    return ln_stats_launch(x, rdt, R, D, Dp, 1e-3f, stat, st);
+    return partials ? ln_stats_finalize_launch(pstat, R, nslot, D, 1e-3f, stat, st)
+                    : ln_stats_launch(x, rdt, R, D, Dp, 1e-3f, stat, st);
   };
   void* xb = ws + P.xb;
   void* h = ws + P.h;
@@ -493,11 +487,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   // against the MX-fp8 weights (W [Np][K8], S [K8/128][Np][4])
   auto enc_gemm = [&](int Np, int K, const void* a, const void* W, const uint8_t* S,
                       const vtd_epilogue* e, double flops) -> int {
-    if (!fp8) {
-      const float* lp = fin_part;
-      fin_part = nullptr;
-      return gemm_launch_ln(M, Np, K, a, K, W, K, dt, e, st, flops, lp, nslot, D, 1e-3f);
-    }
+    if (!fp8) return gemm_launch(M, Np, K, a, K, W, K, dt, e, st, flops);
     const int K8 = k8_of(K);
     int r = quantize_mx8_launch(a, VTD_BF16, R, K, K, K8, q8, K8, s8, P.s8_rows, st);
     if (r) return r;
