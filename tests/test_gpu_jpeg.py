@@ -91,6 +91,46 @@ def test_jpeg_decode_bit_exact_vs_libjpeg_turbo(cuda, monkeypatch, chunk_bits):
                                f"{mine[tuple(bad[0])]} vs {ref[tuple(bad[0])]}")
 
 
+PROG_CASES = [  # progressive (SOF2; libjpeg's simple progression script: DC / AC spectral
+    # selection and successive approximation, every scan with its own Huffman tables)
+    (37, 53, "RGB", dict(quality=75, subsampling=2)),
+    (480, 640, "RGB", dict(quality=85, subsampling=2)),
+    (100, 120, "RGB", dict(quality=95, subsampling=0)),
+    (17, 4, "RGB", dict(quality=60, subsampling=1)),
+    (33, 70, "L", dict(quality=50)),
+    (1, 1, "RGB", dict(quality=80)),
+    (64, 48, "RGB", dict(quality=100, subsampling=1)),
+]
+
+
+def test_jpeg_progressive_bit_exact_vs_libjpeg_turbo(cuda):
+    """Progressive JPEGs decode to libjpeg-turbo's pixels exactly (its jdphuff.c first /
+    refinement scans rebuild the same quantized coefficients; IDCT and colour are shared),
+    batched together with baseline files; and with restart markers (segments decoded in
+    parallel lanes)."""
+    from vision_transformer_detector_amd.preprocess import decode_jpegs
+    files = [_encode(_image(h, w, 50 + i), mode, progressive=True, **kw)
+             for i, (h, w, mode, kw) in enumerate(PROG_CASES)]
+    files.append(_encode(_image(40, 56, 7), quality=85, subsampling=2))       # baseline
+    try:
+        files.append(_encode(_image(72, 88, 8), quality=85, subsampling=2, progressive=True,
+                             restart_marker_rows=1))
+    except TypeError:
+        pass
+    assert all(b"\xff\xc2" in f for f in files[:len(PROG_CASES)])
+    pixels, offsets, sizes = decode_jpegs(files, device=cuda)
+    torch.cuda.synchronize()
+    got = pixels.cpu().numpy()
+    for i, f in enumerate(files):
+        ref = _pil_rgb(f)
+        h, w = sizes[i]
+        assert (h, w) == ref.shape[:2]
+        mine = got[offsets[i]:offsets[i] + h * w * 3].reshape(h, w, 3)
+        bad = np.argwhere(mine != ref)
+        assert bad.size == 0, (f"file {i}: {len(bad)} differing values, first at "
+                               f"{bad[0].tolist()}: {mine[tuple(bad[0])]} vs {ref[tuple(bad[0])]}")
+
+
 def test_jpeg_restart_markers_present():
     data = _restart_case()
     if data is None:
@@ -114,8 +154,8 @@ def test_jpeg_decode_then_resize_matches_host_pipeline(cuda):
 
 def test_jpeg_unsupported_raises(cuda):
     from vision_transformer_detector_amd.preprocess import decode_jpegs
-    prog = _encode(_image(40, 40, 1), quality=80, progressive=True)
-    with pytest.raises(ValueError, match="progressive"):
-        decode_jpegs([prog], device=cuda)
+    cmyk = _encode(_image(40, 40, 1), "CMYK", quality=80)
+    with pytest.raises(ValueError, match="component"):
+        decode_jpegs([cmyk], device=cuda)
     with pytest.raises(ValueError):
         decode_jpegs([b"\x00\x01not a jpeg"], device=cuda)

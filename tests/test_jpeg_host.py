@@ -77,14 +77,30 @@ def test_workspace_plan_dims_and_growth(L):
 
 
 def test_unsupported_flavours_name_the_reason(L):
-    prog = _jpeg(40, 40, quality=80, progressive=True)
-    rc, _ = _info(L, prog)
-    assert rc != 0 and b"progressive" in L.lib.vtd_last_error()
     cmyk = _jpeg(16, 16, "CMYK", quality=80)
     rc, _ = _info(L, cmyk)
     assert rc != 0 and b"component" in L.lib.vtd_last_error()
-    rc, _, _ = _plan(L, [_jpeg(8, 8), prog])
+    rc, _, _ = _plan(L, [_jpeg(8, 8), cmyk])
     assert rc != 0 and b"image 1" in L.lib.vtd_last_error()
+    # arithmetic coding (SOF9): the same file with its SOF0 marker byte changed
+    base = _jpeg(16, 16, quality=80)
+    i = base.index(b"\xff\xc0")
+    arith = base[:i + 1] + b"\xc9" + base[i + 2:]
+    rc, _ = _info(L, arith)
+    assert rc != 0 and b"arithmetic" in L.lib.vtd_last_error()
+
+
+@pytest.mark.parametrize("mode,kw", [("RGB", dict(quality=80, subsampling=2)),
+                                     ("RGB", dict(quality=95, subsampling=0)), ("L", {})])
+def test_progressive_header_walk(L, mode, kw):
+    """Progressive JPEGs (SOF2, several scans with their own Huffman tables) pass the header
+    walk: the dimensions are Pillow's, and the workspace plan grows with the scans."""
+    f = _jpeg(45, 61, mode, progressive=True, **kw)
+    assert f.count(b"\xff\xda") > 1 and b"\xff\xc2" in f
+    rc, dims = _info(L, f)
+    assert rc == 0 and dims[:2] == (45, 61), dims
+    rc, pd, ws = _plan(L, [f, _jpeg(45, 61, mode, **kw)])
+    assert rc == 0 and ws > 0
 
 
 def _with_sof_sampling(f, comp0):

@@ -45,6 +45,7 @@ namespace {
 constexpr int kMaxComp = 3;
 
 struct JpegComp {
+  int id;                   // component identifier of the frame header (scans name it)
   int hs, vs, tq, td, ta;   // sampling factors, quant table, DC / AC Huffman tables
   int bw, bh;               // blocks per row / column of the component plane (MCU-padded)
   int dw, dh;               // downsampled width / height (real samples)
@@ -62,6 +63,9 @@ struct JpegDesc {
   int bpm;                  // blocks per MCU
   int nchunks;              // entropy-decode chunks of this image
   int64_t chunk_base;       // its first chunk in the chunk tables
+  int progressive;          // SOF2: the scans below instead of one sequential scan
+  int nscans;
+  int64_t scan_base;        // its first scan in the scan table
   JpegComp comp[kMaxComp];
   uint16_t q[4][64];        // quantization tables, natural order
   // Huffman tables 0-3 DC, 4-7 AC (jpeg_make_d_derived_tbl): 9-bit lookahead
@@ -77,6 +81,33 @@ __constant__ uint8_t kNatural[64 + 16] = {
     40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36,
     29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54,
     47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
+
+// One derived Huffman table (jdhuff.c d_derived_tbl: 9-bit lookahead, maxcode / valoffset)
+struct DHuff {
+  uint16_t lut[512];
+  int32_t maxcode[18];
+  int32_t valoff[17];
+  uint8_t huffval[256];
+};
+
+// One scan of a progressive image (jdphuff.c): spectral band [ss, se], successive
+// approximation bit positions ah (0: first scan of the band) / al, the restart interval in
+// effect, and the Huffman tables it uses (DC scans: one per scan component; AC scans: h[0]),
+// snapshot at the scan (DHT segments may redefine tables between scans).
+constexpr int kMaxScans = 128;
+struct ProgScan {
+  int ncomp;
+  int comp[kMaxComp];       // frame component indices, in scan order
+  int ss, se, ah, al;
+  int restart;              // MCUs per restart interval, 0: none
+  int nmcu;                 // MCUs of the scan (one block each when ncomp == 1)
+  int64_t raw_off;          // host: entropy-coded data in the file
+  int64_t raw_len;
+  int64_t data_off;         // clean data, bytes from the image's data_off (8-aligned)
+  int data_len;             // clean bytes
+  int nseg, seg_base;       // restart segments: byte starts at segtab[seg_base ...]
+  DHuff h[kMaxComp];
+};
 
 // ------------------------------------------------------------------ host parser
 const uint8_t kZigzagToNatural[64] = {
@@ -136,23 +167,55 @@ bool derive_huffman(const RawHuff& r, bool dc, uint16_t* lut, int32_t* maxcode,
   return true;
 }
 
-// Marker walk of one file: frame, tables, restart interval, scan; fills `d` (offsets
-// excluded) and the entropy-coded data's start `seg` (`seglen` bounds it: the file's rest).
+// End of the entropy-coded data starting at `pos`: the first marker that is not a stuffed
+// 0xFF (FF 00), a fill byte or a restart marker RSTn.
+size_t scan_end(const uint8_t* b, size_t pos, size_t n) {
+  while (pos < n) {
+    const uint8_t* f = static_cast<const uint8_t*>(memchr(b + pos, 0xFF, n - pos));
+    if (!f) return n;
+    const size_t q = f - b;
+    size_t r = q + 1;
+    while (r < n && b[r] == 0xFF) ++r;
+    if (r >= n) return n;
+    if (b[r] == 0x00 || (b[r] >= 0xD0 && b[r] <= 0xD7)) {
+      pos = r + 1;
+      continue;
+    }
+    return q;
+  }
+  return n;
+}
+
+// Marker walk of one file: frame, tables, restart interval, scan(s); fills `d` (offsets
+// excluded).  Sequential images: the entropy-coded data's start `seg` (`seglen` bounds it:
+// the file's rest).  Progressive images (SOF2): every scan into `scans` (when given) with
+// its parameters, the restart interval in effect and, when `derive`, the Huffman tables it
+// uses as they are defined at that scan.
 bool parse_jpeg(const uint8_t* b, size_t n, JpegDesc& d, size_t& seg, size_t& seglen,
-                std::string& err, bool derive = true) {
+                std::string& err, bool derive = true, std::vector<ProgScan>* scans = nullptr) {
   memset(&d, 0, sizeof(d));
+  if (scans) scans->clear();
   if (n < 4 || b[0] != 0xFF || b[1] != 0xD8) { err = "jpeg: no SOI marker"; return false; }
   RawHuff huff[8];
   bool qdef[4] = {}, frame = false;
+  int nscans = 0;
   size_t pos = 2;
   auto u16 = [&](size_t at) { return (int)b[at] << 8 | b[at + 1]; };
   while (true) {
     while (pos < n && b[pos] != 0xFF) ++pos;                  // tolerate junk before markers
     while (pos < n && b[pos] == 0xFF) ++pos;
-    if (pos >= n) { err = "jpeg: no scan"; return false; }
+    if (pos >= n) {
+      if (d.progressive && nscans > 0) break;                 // no EOI: the scans read so far
+      err = "jpeg: no scan";
+      return false;
+    }
     const int m = b[pos++];
     if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;
-    if (m == 0xD9) { err = "jpeg: no scan before EOI"; return false; }
+    if (m == 0xD9) {
+      if (d.progressive && nscans > 0) break;
+      err = "jpeg: no scan before EOI";
+      return false;
+    }
     if (pos + 2 > n) { err = "jpeg: truncated marker"; return false; }
     const int len = u16(pos);
     if (len < 2 || pos + len > n) { err = "jpeg: truncated marker segment"; return false; }
@@ -184,8 +247,10 @@ bool parse_jpeg(const uint8_t* b, size_t n, JpegDesc& d, size_t& seg, size_t& se
         p += count;
         h.present = true;
       }
-    } else if (m == 0xC0 || m == 0xC1) {                      // SOF0 / SOF1: Huffman, sequential
+    } else if (m == 0xC0 || m == 0xC1 || m == 0xC2) {         // SOF0 / 1 / 2: Huffman
+      if (frame) { err = "jpeg: more than one frame"; return false; }
       if (len < 8 || b[s] != 8) { err = "jpeg: only 8-bit samples are supported"; return false; }
+      d.progressive = m == 0xC2;
       d.h = u16(s + 1);
       d.w = u16(s + 3);
       d.nc = b[s + 5];
@@ -196,6 +261,7 @@ bool parse_jpeg(const uint8_t* b, size_t n, JpegDesc& d, size_t& seg, size_t& se
       }
       for (int c = 0; c < d.nc; ++c) {
         JpegComp& jc = d.comp[c];
+        jc.id = b[s + 6 + 3 * c];
         jc.hs = b[s + 7 + 3 * c] >> 4;
         jc.vs = b[s + 7 + 3 * c] & 15;
         jc.tq = b[s + 8 + 3 * c];
@@ -219,10 +285,28 @@ bool parse_jpeg(const uint8_t* b, size_t n, JpegDesc& d, size_t& seg, size_t& se
         err = "jpeg: unsupported subsampling 4:4:0 (4:4:4, 4:2:2, 4:2:0 only)";
         return false;
       }
+      // derived geometry
+      if (d.nc == 1) {
+        d.mcux = (d.w + 7) / 8;
+        d.mcuy = (d.h + 7) / 8;
+      } else {
+        d.mcux = (d.w + 8 * d.hmax - 1) / (8 * d.hmax);
+        d.mcuy = (d.h + 8 * d.vmax - 1) / (8 * d.vmax);
+      }
+      for (int c = 0; c < d.nc; ++c) {
+        JpegComp& jc = d.comp[c];
+        d.bpm += jc.hs * jc.vs;
+        jc.bw = d.mcux * jc.hs;
+        jc.bh = d.mcuy * jc.vs;
+        jc.dw = (d.w * jc.hs + d.hmax - 1) / d.hmax;
+        jc.dh = (d.h * jc.vs + d.vmax - 1) / d.vmax;
+        jc.coef_off = d.nblocks;
+        d.nblocks += jc.bw * jc.bh;
+      }
       frame = true;
-    } else if (m >= 0xC2 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
-      err = m == 0xC2 ? "jpeg: progressive JPEG is not supported by the device decoder"
-                      : "jpeg: only baseline / extended sequential Huffman JPEG is supported";
+    } else if (m >= 0xC3 && m <= 0xCF && m != 0xC4 && m != 0xC8 && m != 0xCC) {
+      err = "jpeg: only Huffman-coded baseline / extended sequential / progressive JPEG is "
+            "supported (arithmetic-coded, lossless and hierarchical are not)";
       return false;
     } else if (m == 0xDD) {                                   // DRI
       if (len < 4) { err = "jpeg: truncated DRI segment"; return false; }
@@ -233,51 +317,98 @@ bool parse_jpeg(const uint8_t* b, size_t n, JpegDesc& d, size_t& seg, size_t& se
       if (!frame) { err = "jpeg: scan before frame"; return false; }
       if (len < 3) { err = "jpeg: truncated SOS segment"; return false; }
       const int ns = b[s];
-      if (ns != d.nc || len != 6 + 2 * ns) {
-        err = "jpeg: only single-scan images with all components interleaved are supported";
-        return false;
-      }
+      if (ns < 1 || ns > d.nc || len != 6 + 2 * ns) { err = "jpeg: bad SOS segment"; return false; }
+      int idx[kMaxComp], td[kMaxComp], ta[kMaxComp];
       for (int i = 0; i < ns; ++i) {
         const int cid = b[s + 1 + 2 * i], tbl = b[s + 2 + 2 * i];
-        (void)cid;
-        d.comp[i].td = tbl >> 4;
-        d.comp[i].ta = tbl & 15;
-        if (d.comp[i].td > 3 || d.comp[i].ta > 3) { err = "jpeg: bad scan table ids"; return false; }
+        idx[i] = -1;
+        for (int c = 0; c < d.nc; ++c)
+          if (d.comp[c].id == cid) idx[i] = c;
+        for (int j = 0; j < i; ++j)
+          if (idx[j] == idx[i]) idx[i] = -1;
+        if (idx[i] < 0) { err = "jpeg: scan names an unknown or repeated component"; return false; }
+        td[i] = tbl >> 4;
+        ta[i] = tbl & 15;
+        if (td[i] > 3 || ta[i] > 3) { err = "jpeg: bad scan table ids"; return false; }
       }
       const int ss = b[s + 1 + 2 * ns], se = b[s + 2 + 2 * ns], ahal = b[s + 3 + 2 * ns];
-      if (ss != 0 || se != 63 || ahal != 0) { err = "jpeg: not a sequential scan"; return false; }
-      seg = e;
-      // the scan's end (the first marker other than RSTn) is found while unstuffing; here
-      // the rest of the file bounds it
-      seglen = n - seg;
-      break;
+      if (!d.progressive) {
+        if (ns != d.nc) {
+          err = "jpeg: only single-scan images with all components interleaved are supported";
+          return false;
+        }
+        for (int i = 0; i < ns; ++i) {
+          if (idx[i] != i) { err = "jpeg: scan component order differs from the frame's"; return false; }
+          d.comp[i].td = td[i];
+          d.comp[i].ta = ta[i];
+        }
+        if (ss != 0 || se != 63 || ahal != 0) { err = "jpeg: not a sequential scan"; return false; }
+        seg = e;
+        // the scan's end (the first marker other than RSTn) is found while unstuffing; here
+        // the rest of the file bounds it
+        seglen = n - seg;
+        break;
+      }
+      // progressive scan (the checks of jdphuff.c start_pass_phuff_decoder)
+      const int ah = ahal >> 4, al = ahal & 15;
+      const bool dc = ss == 0;
+      if ((dc && se != 0) || (!dc && (se < ss || se > 63 || ns != 1)) || al > 13 ||
+          (ah != 0 && al != ah - 1)) {
+        err = "jpeg: bad progressive scan parameters";
+        return false;
+      }
+      if (nscans >= kMaxScans) { err = "jpeg: too many scans"; return false; }
+      // tables this scan reads: DC first scans one DC table per component, AC scans one AC
+      // table; DC refinement scans none
+      const int ntab = dc ? (ah == 0 ? ns : 0) : 1;
+      for (int i = 0; i < ntab; ++i) {
+        const int t = dc ? td[i] : ta[0] + 4;
+        if (!huff[t].present) { err = "jpeg: missing Huffman table"; return false; }
+      }
+      const size_t end = scan_end(b, e, n);
+      if (scans) {
+        scans->emplace_back();
+        ProgScan& ps = scans->back();
+        memset(&ps, 0, sizeof(ps));
+        ps.ncomp = ns;
+        for (int i = 0; i < ns; ++i) ps.comp[i] = idx[i];
+        ps.ss = ss;
+        ps.se = se;
+        ps.ah = ah;
+        ps.al = al;
+        ps.restart = d.restart;
+        if (ns == 1) {
+          const JpegComp& jc = d.comp[idx[0]];
+          ps.nmcu = ((jc.dw + 7) / 8) * ((jc.dh + 7) / 8);
+        } else {
+          ps.nmcu = d.mcux * d.mcuy;
+        }
+        ps.nseg = ps.restart ? (ps.nmcu + ps.restart - 1) / ps.restart : 1;
+        ps.raw_off = (int64_t)e;
+        ps.raw_len = (int64_t)(end - e);
+        for (int i = 0; i < ntab && derive; ++i) {
+          const int t = dc ? td[i] : ta[0] + 4;
+          if (!derive_huffman(huff[t], dc, ps.h[i].lut, ps.h[i].maxcode, ps.h[i].valoff,
+                              ps.h[i].huffval, err))
+            return false;
+        }
+      }
+      ++nscans;
+      pos = end;
+      continue;
     }
     pos = e;
   }
-  // derived geometry and tables
-  if (d.nc == 1) {
-    d.mcux = (d.w + 7) / 8;
-    d.mcuy = (d.h + 7) / 8;
-  } else {
-    d.mcux = (d.w + 8 * d.hmax - 1) / (8 * d.hmax);
-    d.mcuy = (d.h + 8 * d.vmax - 1) / (8 * d.vmax);
+  for (int c = 0; c < d.nc; ++c)
+    if (!qdef[d.comp[c].tq]) { err = "jpeg: missing quantization table"; return false; }
+  if (d.progressive) {
+    d.nscans = nscans;
+    return true;
   }
-  d.nblocks = 0;
-  d.bpm = 0;
-  for (int c = 0; c < d.nc; ++c) {
-    JpegComp& jc = d.comp[c];
-    d.bpm += jc.hs * jc.vs;
-    if (!qdef[jc.tq]) { err = "jpeg: missing quantization table"; return false; }
-    jc.bw = d.mcux * jc.hs;
-    jc.bh = d.mcuy * jc.vs;
-    jc.dw = (d.w * jc.hs + d.hmax - 1) / d.hmax;
-    jc.dh = (d.h * jc.vs + d.vmax - 1) / d.vmax;
-    jc.coef_off = d.nblocks;
-    d.nblocks += jc.bw * jc.bh;
-    for (int t : {jc.td, jc.ta + 4}) {
+  for (int c = 0; c < d.nc; ++c)
+    for (int t : {d.comp[c].td, d.comp[c].ta + 4}) {
       if (!huff[t].present) { err = "jpeg: missing Huffman table"; return false; }
     }
-  }
   for (int t = 0; t < 8 && derive; ++t)
     if (huff[t].present &&
         !derive_huffman(huff[t], t < 4, d.lut[t], d.maxcode[t], d.valoff[t], d.huffval[t], err))
@@ -615,6 +746,172 @@ __global__ __launch_bounds__(kThreads) void jpeg_huffman_kernel(const JpegDesc* 
   }
 }
 
+// ------------------------------------------------------------------ device: progressive
+// Progressive images (SOF2), jdphuff.c: the scans run in file order, each adding to the
+// quantized coefficients the sequential path writes in one pass (same layout, so the IDCT
+// and colour kernels are shared).  One 64-thread workgroup per image; a scan's restart
+// segments are independent (EOBRUN and the DC predictions restart with each), so lane l takes
+// segments l, l + 64, ...; a scan without restarts is one lane's serial walk (Huffman decoding
+// is sequential per segment; progressive files are a small share of a dataset, and this path
+// is about exactness first).  __syncthreads between scans orders each refinement after the
+// scan before it.
+__device__ __forceinline__ int huff_decode_d(Bits& br, const DHuff& T) {
+  const int e = T.lut[br.peek(9)];
+  if (e) {
+    br.skip(e >> 8);
+    return e & 0xFF;
+  }
+  int l = 10;
+  int code = (int)br.peek(10);
+  while (code > T.maxcode[l]) {
+    ++l;
+    if (l > 16) {                // corrupt data: consume and return 0 (jdhuff.c warns)
+      br.skip(16);
+      return 0;
+    }
+    code = (int)br.peek(l);
+  }
+  br.skip(l);
+  return T.huffval[(code + T.valoff[l]) & 0xFF];
+}
+
+// the refinement of jdphuff.c decode_mcu_AC_refine for an already-nonzero coefficient
+__device__ __forceinline__ void ac_correct(Bits& br, int16_t* c, int p1, int m1) {
+  if (br.get(1)) {
+    if ((*c & p1) == 0) *c = (int16_t)(*c + (*c >= 0 ? p1 : m1));
+  }
+}
+
+__device__ void prog_segment(const JpegDesc& d, const ProgScan& S, const DHuff* H,
+                             const uint8_t* nat, const uint8_t* data, const int* segtab, int seg,
+                             int16_t* coefs) {
+  const int per = S.restart ? S.restart : S.nmcu;
+  const int m0 = seg * per, m1 = min(m0 + per, S.nmcu);
+  const int b0 = segtab[S.seg_base + seg];
+  const int b1 = seg + 1 < S.nseg ? segtab[S.seg_base + seg + 1] : S.data_len;
+  Bits br;
+  br.w = reinterpret_cast<const uint32_t*>(data + d.data_off + S.data_off);
+  br.end = b1 * 8;
+  br.seek(b0 * 8);
+  int eobrun = 0;
+  Comp3 pred;
+  pred.set(0, 0, 0);
+  const int p1 = 1 << S.al, m1_ = -1 * (1 << S.al);
+  const bool dc = S.ss == 0, refine = S.ah != 0;
+  for (int mcu = m0; mcu < m1; ++mcu) {
+    // blocks of this MCU: (scan component index, block pointer)
+    int nb = 0;
+    int16_t* blk[kMaxBpm];
+    int bci[kMaxBpm];
+    if (S.ncomp == 1) {
+      const JpegComp& jc = d.comp[S.comp[0]];
+      const int bwp = (jc.dw + 7) / 8;
+      const int by = mcu / bwp, bx = mcu - by * bwp;
+      blk[0] = coefs + (d.coef_base + jc.coef_off + (int64_t)by * jc.bw + bx) * 64;
+      bci[0] = 0;
+      nb = 1;
+    } else {
+      const int my = mcu / d.mcux, mx = mcu - my * d.mcux;
+      for (int ci = 0; ci < S.ncomp; ++ci) {
+        const JpegComp& jc = d.comp[S.comp[ci]];
+        for (int v = 0; v < jc.vs; ++v)
+          for (int h = 0; h < jc.hs; ++h) {
+            blk[nb] = coefs + (d.coef_base + jc.coef_off + (int64_t)(my * jc.vs + v) * jc.bw +
+                               mx * jc.hs + h) * 64;
+            bci[nb++] = ci;
+          }
+      }
+    }
+    for (int bi = 0; bi < nb; ++bi) {
+      int16_t* B = blk[bi];
+      if (dc && !refine) {                                 // decode_mcu_DC_first
+        int sv = huff_decode_d(br, H[bci[bi]]);
+        if (sv) sv = huff_extend(br.get(sv), sv);
+        const int v = pred.add(bci[bi], sv);
+        B[0] = (int16_t)((unsigned)v << S.al);
+      } else if (dc) {                                     // decode_mcu_DC_refine
+        if (br.get(1)) B[0] = (int16_t)(B[0] | p1);
+      } else if (!refine) {                                // decode_mcu_AC_first
+        if (eobrun > 0) {
+          --eobrun;
+          continue;
+        }
+        for (int k = S.ss; k <= S.se; ++k) {
+          const int rs = huff_decode_d(br, H[0]);
+          int r = rs >> 4, sv = rs & 15;
+          if (sv) {
+            k += r;
+            sv = huff_extend(br.get(sv), sv);
+            B[nat[k]] = (int16_t)((unsigned)sv << S.al);
+          } else if (r == 15) {
+            k += 15;
+          } else {
+            eobrun = 1 << r;
+            if (r) eobrun += br.get(r);
+            --eobrun;
+            break;
+          }
+        }
+      } else {                                             // decode_mcu_AC_refine
+        int k = S.ss;
+        if (eobrun == 0) {
+          for (; k <= S.se; ++k) {
+            const int rs = huff_decode_d(br, H[0]);
+            int r = rs >> 4, sv = rs & 15;
+            if (sv) {
+              sv = br.get(1) ? p1 : m1_;
+            } else if (r != 15) {
+              eobrun = 1 << r;
+              if (r) eobrun += br.get(r);
+              break;
+            }
+            do {
+              int16_t* c = B + nat[k];
+              if (*c != 0) {
+                ac_correct(br, c, p1, m1_);
+              } else {
+                if (--r < 0) break;
+              }
+              ++k;
+            } while (k <= S.se);
+            if (sv) B[nat[k]] = (int16_t)sv;
+          }
+        }
+        if (eobrun > 0) {
+          for (; k <= S.se; ++k) {
+            int16_t* c = B + nat[k];
+            if (*c != 0) ac_correct(br, c, p1, m1_);
+          }
+          --eobrun;
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void jpeg_progressive_kernel(const JpegDesc* __restrict__ descs,
+                                                              const uint8_t* __restrict__ data,
+                                                              const ProgScan* __restrict__ scans,
+                                                              const int* __restrict__ segtab,
+                                                              int16_t* __restrict__ coefs) {
+  const JpegDesc& d = descs[blockIdx.x];
+  if (!d.progressive) return;
+  __shared__ DHuff H[kMaxComp];
+  __shared__ uint8_t nat[64 + 16];
+  const int t = threadIdx.x;
+  for (int i = t; i < 64 + 16; i += 64) nat[i] = kNatural[i];
+  for (int sc = 0; sc < d.nscans; ++sc) {
+    const ProgScan& S = scans[d.scan_base + sc];
+    __syncthreads();                                       // previous scan done, tables free
+    const int ntab = S.ss == 0 ? (S.ah == 0 ? S.ncomp : 0) : 1;
+    const int words = ntab * (int)(sizeof(DHuff) / 4);
+    for (int i = t; i < words; i += 64)
+      reinterpret_cast<uint32_t*>(H)[i] = reinterpret_cast<const uint32_t*>(S.h)[i];
+    __syncthreads();
+    for (int sg = t; sg < S.nseg; sg += 64) prog_segment(d, S, H, nat, data, segtab, sg, coefs);
+  }
+}
+
 // ------------------------------------------------------------------ device: IDCT
 constexpr int32_t FIX_0_298631336 = 2446, FIX_0_390180644 = 3196, FIX_0_541196100 = 4433,
                   FIX_0_765366865 = 6270, FIX_0_899976223 = 7373, FIX_1_175875602 = 9633,
@@ -864,7 +1161,7 @@ Staging& staging() {
 }
 
 struct Layout {
-  size_t desc, data, chunk, state, coef, plane, total;
+  size_t desc, data, chunk, scan, segtab, state, coef, plane, total;
 };
 
 // Restart segments of an image (1 without DRI) and the chunk-table bound: the chunking
@@ -900,27 +1197,47 @@ void parallel_for(int n, int per_thread_min, F&& f) {
 // the decode) and lays out the workspace.  The first failing image (lowest index) is
 // reported.
 int plan(const uint8_t* const* jpegs, const size_t* lens, int n, std::vector<JpegDesc>* descs,
-         std::vector<size_t>* segs, std::vector<size_t>* seglens, int32_t* dims, Layout& L) {
+         std::vector<size_t>* segs, std::vector<size_t>* seglens, int32_t* dims, Layout& L,
+         std::vector<std::vector<ProgScan>>* pscans = nullptr) {
   VTD_CHECK_ARG(jpegs && lens && n > 0, "jpeg: bad arguments");
   for (int i = 0; i < n; ++i) VTD_CHECK_ARG(jpegs[i] && lens[i] > 0, "jpeg: null / empty image");
   static thread_local std::vector<JpegDesc> local;   // reused: no page faults per call
+  static thread_local std::vector<std::vector<ProgScan>> local_scans;
   std::vector<JpegDesc>& D = descs ? *descs : local;
+  std::vector<std::vector<ProgScan>>& P = pscans ? *pscans : local_scans;
   D.resize(n);
+  P.resize(n);
   std::vector<size_t> sg(n), sl(n);
   std::vector<std::string> errs(n);
   std::vector<char> ok(n, 0);
   const bool derive = descs != nullptr;
   parallel_for(n, 2048, [&](int i0, int i1) {   // ~0.7 us per image: threads only for huge batches
     for (int i = i0; i < i1; ++i)
-      ok[i] = parse_jpeg(jpegs[i], lens[i], D[i], sg[i], sl[i], errs[i], derive);
+      ok[i] = parse_jpeg(jpegs[i], lens[i], D[i], sg[i], sl[i], errs[i], derive, &P[i]);
   });
-  size_t data = 0, coef = 0, plane = 0, chunks = 0;
+  size_t data = 0, coef = 0, plane = 0, chunks = 0, nscan = 0, nseg = 0;
   for (int i = 0; i < n; ++i) {
     if (!ok[i]) return fail(VTD_ERR_UNSUPPORTED, errs[i] + " (image " + std::to_string(i) + ")");
     JpegDesc& d = D[i];
-    VTD_CHECK_ARG(sl[i] < (1u << 27), "jpeg: scan too large (bit offsets are 31-bit)");
     d.data_off = (int64_t)data;
-    data += align256(sl[i] + 8);
+    if (d.progressive) {
+      // every scan's clean data 8-aligned inside the image's data region (+ 8 zero bytes)
+      size_t cur = 0;
+      d.scan_base = (int64_t)nscan;
+      for (ProgScan& ps : P[i]) {
+        VTD_CHECK_ARG(ps.raw_len < (1 << 27), "jpeg: scan too large (bit offsets are 31-bit)");
+        ps.data_off = (int64_t)cur;
+        cur += (size_t)(ps.raw_len + 8 + 7) / 8 * 8;
+        ps.seg_base = (int)nseg;
+        nseg += ps.nseg;
+      }
+      nscan += P[i].size();
+      data += align256(cur);
+      d.nchunks = 0;
+    } else {
+      VTD_CHECK_ARG(sl[i] < (1u << 27), "jpeg: scan too large (bit offsets are 31-bit)");
+      data += align256(sl[i] + 8);
+    }
     for (int c = 0; c < d.nc; ++c) {
       d.comp[c].plane_off = (int64_t)plane;
       plane += align256((size_t)d.comp[c].bw * 8 * d.comp[c].bh * 8);
@@ -928,7 +1245,7 @@ int plan(const uint8_t* const* jpegs, const size_t* lens, int n, std::vector<Jpe
     d.coef_base = (int64_t)(coef / 128);
     coef += align256((size_t)d.nblocks * 128);
     d.chunk_base = (int64_t)chunks;
-    chunks += kThreads + segments_of(d);
+    if (!d.progressive) chunks += kThreads + segments_of(d);
     if (dims) {
       dims[2 * i] = d.h;
       dims[2 * i + 1] = d.w;
@@ -939,7 +1256,9 @@ int plan(const uint8_t* const* jpegs, const size_t* lens, int n, std::vector<Jpe
   L.desc = 0;
   L.data = align256((size_t)n * sizeof(JpegDesc));
   L.chunk = L.data + data;
-  L.state = L.chunk + align256(chunks * sizeof(JpegChunk));
+  L.scan = L.chunk + align256(chunks * sizeof(JpegChunk));
+  L.segtab = L.scan + align256(nscan * sizeof(ProgScan));
+  L.state = L.segtab + align256(nseg * sizeof(int));
   L.coef = L.state + align256(chunks * sizeof(JpegChunkState));
   L.plane = L.coef + coef;
   L.total = L.plane + plane;
@@ -1041,21 +1360,24 @@ extern "C" int vtd_jpeg_decode(const uint8_t* const* jpegs, const size_t* lens, 
   // reused across calls (no page faults per call); a named reference, because the worker
   // threads below must see this thread's vector, not their own thread_local instance
   static thread_local std::vector<JpegDesc> descs_tls;
+  static thread_local std::vector<std::vector<ProgScan>> scans_tls;
   std::vector<JpegDesc>& descs = descs_tls;
+  std::vector<std::vector<ProgScan>>& pscans = scans_tls;
   std::vector<size_t> segs, seglens;
   Layout L;
   // VTD_JPEG_TIMING=1: host phase times of each call on stderr (diagnostics)
   static const bool timing = getenv("VTD_JPEG_TIMING") != nullptr;
   auto now = [] { return std::chrono::steady_clock::now(); };
   const auto t0 = now();
-  int rc = plan(jpegs, lens, n, &descs, &segs, &seglens, nullptr, L);
+  int rc = plan(jpegs, lens, n, &descs, &segs, &seglens, nullptr, L, &pscans);
   const auto t1 = now();
   if (rc != VTD_OK) return rc;
   if (workspace_bytes < L.total)
     return fail(VTD_ERR_WORKSPACE, "jpeg_decode: workspace too small");
   hipStream_t st = static_cast<hipStream_t>(stream);
-  int max_blocks = 0, max_h = 0, max_w = 0;
+  int max_blocks = 0, max_h = 0, max_w = 0, nprog = 0;
   for (int i = 0; i < n; ++i) {
+    nprog += descs[i].progressive;
     descs[i].out_off = out_offsets[i];
     max_blocks = std::max(max_blocks, descs[i].nblocks);
     max_h = std::max(max_h, descs[i].h);
@@ -1085,10 +1407,25 @@ extern "C" int vtd_jpeg_decode(const uint8_t* const* jpegs, const size_t* lens, 
   JpegChunk* chunks = reinterpret_cast<JpegChunk*>(sg.host + L.chunk);
   size_t raw = 0;
   for (int i = 0; i < n; ++i) raw += seglens[i];
+  ProgScan* scan_tab = reinterpret_cast<ProgScan*>(sg.host + L.scan);
+  int* segtab = reinterpret_cast<int*>(sg.host + L.segtab);
   auto work = [&](int i0, int i1) {
     std::vector<size_t> starts;
     for (int i = i0; i < i1; ++i) {
       JpegDesc& d = descs[i];
+      if (d.progressive) {                     // each scan: unstuff + its restart segments
+        for (size_t k = 0; k < pscans[i].size(); ++k) {
+          ProgScan& ps = pscans[i][k];
+          uint8_t* clean = sg.host + L.data + d.data_off + ps.data_off;
+          const size_t len = unstuff(jpegs[i] + ps.raw_off, (size_t)ps.raw_len, clean, ps.nseg,
+                                     starts);
+          memset(clean + len, 0, 8);
+          ps.data_len = (int)len;
+          for (int g = 0; g < ps.nseg; ++g) segtab[ps.seg_base + g] = (int)starts[g];
+          memcpy(scan_tab + d.scan_base + k, &ps, sizeof(ProgScan));
+        }
+        continue;
+      }
       uint8_t* clean = sg.host + L.data + d.data_off;
       const size_t len = unstuff(jpegs[i] + segs[i], seglens[i], clean, segments_of(d), starts);
       memset(clean + len, 0, 8);
@@ -1097,6 +1434,9 @@ extern "C" int vtd_jpeg_decode(const uint8_t* const* jpegs, const size_t* lens, 
     }
   };
   const auto t2 = now();
+  for (int i = 0; i < n; ++i)
+    if (descs[i].progressive)
+      for (const ProgScan& ps : pscans[i]) raw += (size_t)ps.raw_len;
   parallel_for(n, (int)std::max<size_t>(1, (size_t)n * (1u << 20) / std::max<size_t>(raw, 1)),
                work);
   if (timing) fprintf(stderr, "[vtd_jpeg] unstuff %.3f ms\n",
@@ -1121,6 +1461,13 @@ extern "C" int vtd_jpeg_decode(const uint8_t* const* jpegs, const size_t* lens, 
                      reinterpret_cast<JpegChunkState*>(ws + L.state),
                      reinterpret_cast<int16_t*>(ws + L.coef));
   VTD_LAUNCH_CHECK("jpeg_huffman");
+  if (nprog) {
+    hipLaunchKernelGGL(jpeg_progressive_kernel, dim3(n), dim3(64), 0, st, d_desc, ws + L.data,
+                       reinterpret_cast<const ProgScan*>(ws + L.scan),
+                       reinterpret_cast<const int*>(ws + L.segtab),
+                       reinterpret_cast<int16_t*>(ws + L.coef));
+    VTD_LAUNCH_CHECK("jpeg_progressive");
+  }
   const auto t5 = now();
   hipLaunchKernelGGL(jpeg_idct_kernel, dim3((max_blocks + 255) / 256, n), dim3(256), 0, st,
                      d_desc, reinterpret_cast<const int16_t*>(ws + L.coef), ws + L.plane);
