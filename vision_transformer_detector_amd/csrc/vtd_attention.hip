@@ -259,20 +259,32 @@ struct AttnBf16Cfg {
 // each) the amax of the bf16-rounded values -> E8M0 scale -> e4m3 bytes, exactly what
 // vtd_quantize_mx8 makes of the bf16 output (layout in vtd_mx8.hip: q[row][ldo] bytes,
 // s[k / 128][s_rows][4]).
+// Grid: one workgroup per (query block of NWG x 32 queries, head, image), 1-D.  The query
+// blocks of one (image, head) stream the same K / V chunks, so workgroup ids are remapped
+// XCD-aware (xcd_remap != 0): blocks b, b + 8, ... share an XCD and walk one contiguous range
+// of (pair, query block) ids, so a pair's query blocks run on one XCD and read its K / V
+// through that XCD's L2 once instead of once per XCD from beyond it.
 template <int DKP, int NWG, bool MX8 = false>
 __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void attention_bf16_kernel(
     const bf16_t* __restrict__ qkv, int N, int heads, int ldqkv, float scale_log2,
-    bf16_t* __restrict__ out, int ldo, uint8_t* __restrict__ s8 = nullptr, int64_t s_rows = 0) {
+    bf16_t* __restrict__ out, int ldo, uint8_t* __restrict__ s8, int64_t s_rows, int nqb,
+    int xcd_remap) {
   using C = AttnBf16Cfg<DKP>;
   typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   constexpr int nthreads = 64 * NWG;
   const int lane = tid & 63, wave = tid >> 6, half = lane >> 5, col = lane & 31;
-  const int h = blockIdx.y, b = blockIdx.z;
+  int v = blockIdx.x;
+  if (xcd_remap) {
+    const int G = gridDim.x, xcd = v & 7, q8 = G >> 3, r8 = G & 7;
+    v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (v >> 3);
+  }
+  const int pair = v / nqb, qb = v - pair * nqb;
+  const int b = pair / heads, h = pair - b * heads;
   const int inner = heads * DKP;
   const int64_t row0 = (int64_t)b * N;
-  const int q0 = (blockIdx.x * NWG + wave) * 32;
+  const int q0 = (qb * NWG + wave) * 32;
   const bool active = q0 < N;
 
   bf16x8 qf[C::KSTEPS];
@@ -751,17 +763,23 @@ int launch_bf16_v2(const void* qkv, int B, int N, int heads, int ldqkv, float sc
                    void* out, int ldo, hipStream_t stream, uint8_t* s8 = nullptr,
                    int64_t s_rows = 0) {
   using C = AttnBf16Cfg<DKP>;
-  const int nq = (N + 31) / 32;
-  dim3 grid((nq + NWG - 1) / NWG, heads, B);
+  const int nq = (N + 31) / 32, nqb = (nq + NWG - 1) / NWG;
+  VTD_CHECK_ARG((int64_t)nqb * heads * B < INT32_MAX, "attention: grid too large");
+  const dim3 grid(nqb * heads * B);
   static std::once_flag once[kMaxDevices];
   once_per_device(once, [] {
     (void)hipFuncSetAttribute(
         reinterpret_cast<const void*>(&attention_bf16_kernel<DKP, NWG, MX8>),
         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * C::BUF);
   });
+  // XCD-aware order: C3 attention 382.5-383.2 vs 384.0-384.2 us per launch, forward
+  // 1,812-1,813 vs 1,783-1,790 img/s (profiles/r03_attn_xcd_order_ab.log); the kernel is
+  // VALU-bound, its K / V re-reads were mostly served beyond L2 at no visible cost
+  const int xcd_remap = 1;
   hipLaunchKernelGGL((attention_bf16_kernel<DKP, NWG, MX8>), grid, dim3(64 * NWG), 2 * C::BUF,
                      stream, static_cast<const bf16_t*>(qkv), N, heads, ldqkv,
-                     scale * 1.4426950408889634f, static_cast<bf16_t*>(out), ldo, s8, s_rows);
+                     scale * 1.4426950408889634f, static_cast<bf16_t*>(out), ldo, s8, s_rows,
+                     nqb, xcd_remap);
   VTD_LAUNCH_CHECK("attention_bf16");
   return VTD_OK;
 }
