@@ -340,16 +340,20 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
   // per-lane tr-read address pieces: key offset within a 4-key block, d offset
   const int tr_key = 4 * half + ((lane & 15) >> 2);
   const int tr_d = ((lane >> 4) & 1) * 16 + (lane & 3) * 4;
-  for (int c = 0; c < nchunks; ++c) {
+  // one key chunk; LAST = the final chunk (possibly ragged: runtime key-block count and
+  // mask, no next-chunk load): every other chunk is full, so its block loop and mask are
+  // compile-time (no per-chunk branches)
+  auto chunk = [&](int c, auto last_tag) {
+    constexpr bool LAST = decltype(last_tag)::value;
     const int kv0 = c * C::KC;
-    if (c + 1 < nchunks) gload(kv0 + C::KC);
+    if (!LAST) gload(kv0 + C::KC);
     if (active) {
       const char* kl = smem + (c & 1) * C::BUF;
       const char* vl = kl + C::KC * C::KS;
       // 32-key blocks of this chunk holding at least one key (the last chunk may be
       // ragged: N = 196 leaves 4 keys in it, one block)
-      const int nkb = min(2, (N - kv0 + 31) >> 5);
-      const bool ragged = kv0 + C::KC > N;
+      const int nkb = LAST ? min(2, (N - kv0 + 31) >> 5) : 2;
+      const bool ragged = LAST && kv0 + C::KC > N;
       f32x16 s[2];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
@@ -437,9 +441,11 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
           }
         }
     }
-    if (c + 1 < nchunks) swrite((c + 1) & 1);
+    if (!LAST) swrite((c + 1) & 1);
     __syncthreads();
-  }
+  };
+  for (int c = 0; c + 1 < nchunks; ++c) chunk(c, std::false_type{});
+  chunk(nchunks - 1, std::true_type{});
   if (!active) return;
   const float inv = 1.f / (l_run + __shfl_xor(l_run, 32));
   const int q = q0 + col;
