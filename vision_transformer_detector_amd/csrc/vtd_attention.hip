@@ -385,7 +385,7 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
 #pragma unroll
           for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
         }
-      mx = fmaxf(mx, __shfl_xor(mx, 32)) * scale_log2;
+      mx = pair_max(mx) * scale_log2;                  // lane l ^ 32 holds the other keys
       // deferred rescale (running max in log2 units): the accumulators are rescaled only
       // when some lane's max grows by more than 8, so exp2 arguments stay <= 8 (P <= 256,
       // exact in the bf16 P operand's range, l and O in fp32); the final 1/l normalises
@@ -447,7 +447,7 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
   for (int c = 0; c + 1 < nchunks; ++c) chunk(c, std::false_type{});
   chunk(nchunks - 1, std::true_type{});
   if (!active) return;
-  const float inv = 1.f / (l_run + __shfl_xor(l_run, 32));
+  const float inv = 1.f / pair_sum(l_run);
   const int q = q0 + col;
   if constexpr (!MX8 && DKP == 64) {
     // bf16 output through LDS (free after the loop's last barrier): a lane holds 16-B
@@ -484,7 +484,7 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
         v[i] = bf16_round(o[db][i] * inv);
         amax = fmaxf(amax, fabsf(v[i]));
       }
-      amax = fmaxf(amax, __shfl_xor(amax, 32));
+      amax = pair_max(amax);
       const int E = mx8_exponent(amax);
       const float sinv = __uint_as_float((uint32_t)(127 - E) << 23);     // 2^-E, exact
 #pragma unroll
