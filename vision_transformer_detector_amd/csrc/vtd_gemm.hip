@@ -172,6 +172,8 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
   constexpr bool OUT_BF16 = (EPI & 4) != 0;
   constexpr bool RESID = (EPI & 8) != 0;
   constexpr bool NOBIAS = (EPI & EPI_PARTIAL) != 0;   // split-K partial: raw fp32 sums
+  constexpr bool LNF = (EPI & EPI_LNF) != 0, STAT = (EPI & EPI_STAT) != 0;
+  constexpr bool F8O = (EPI & EPI_F8O) != 0;
   constexpr int ES = 68;
   constexpr int NB = PR / 16;            // accumulator row blocks per pass
   constexpr int NIT = PR / 8;            // row-vector iterations per pass
@@ -183,7 +185,7 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
     b1 = *reinterpret_cast<const f32x4*>(e.bias + n_base + c8 + 4);
   }
   f32x4 cs0 = {}, cs1 = {};
-  if (e.lnstat) {
+  if constexpr (LNF) {
     cs0 = *reinterpret_cast<const f32x4*>(e.colsum + n_base + c8);
     cs1 = *reinterpret_cast<const f32x4*>(e.colsum + n_base + c8 + 4);
   }
@@ -209,7 +211,7 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
       const int row = it * 8 + rsub;
       f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + row * ES + c8);
       f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + row * ES + c8 + 4);
-      if (e.lnstat) epi_lnfold8(e, lst, m_base + p * PR + row, p * PR + row, cs0, cs1, v0, v1);
+      if constexpr (LNF) epi_lnfold8(e, lst, m_base + p * PR + row, p * PR + row, cs0, cs1, v0, v1);
       v0 += b0;
       v1 += b1;
       if (e.rowadd) epi_rowadd8(e, m_base + p * PR + row, n_base + c8, v0, v1);
@@ -221,7 +223,7 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
       if (e.out2) epi_out2_8(e, m_base + p * PR + row, n_base + c8, v0, v1);
       const int64_t idx = (int64_t)(m_base + p * PR + row) * e.ldo + n_base + c8;
       if constexpr (OUT_BF16) {
-        if (e.out_dtype == VTD_FP8) {
+        if constexpr (F8O) {
           // the next MX GEMM's operand: a 32-column block = 4 consecutive lanes (c8 / 8
           // = 0..3 or 4..7), block amax by DPP quad xor 1 / xor 2; bf16-rounded values so
           // the bytes equal vtd_quantize_mx8 of the bf16 output
@@ -250,7 +252,7 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
         const i32x4 o = {(int)pack_bf16x2(v0[0], v0[1]), (int)pack_bf16x2(v0[2], v0[3]),
                          (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
         store_out16(static_cast<bf16_t*>(e.out) + idx, o);
-        if (e.statout) {           // the row's 64 columns live in 8 consecutive lanes
+        if constexpr (STAT) {      // the row's 64 columns live in 8 consecutive lanes
           // block mean, then the centred sum of squares (DPP sums, no LDS traffic)
           const float mean = sum8_dpp(bf16x8_sum(o)) * (1.f / 64.f);
           const float m2 = sum8_dpp(bf16x8_m2(o, mean));
@@ -522,6 +524,7 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
   constexpr int ACT = EPI & 3;
   constexpr bool OUT_BF16 = (EPI & 4) != 0;
   constexpr bool RESID = (EPI & 8) != 0;
+  constexpr bool LNF = (EPI & EPI_LNF) != 0, STAT = (EPI & EPI_STAT) != 0;
   const int fr = lane & 15, fg = lane >> 4;
   f32x4 bias[2][2], cs[2][2] = {};
 #pragma unroll
@@ -529,7 +532,7 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       bias[jp][h] = *reinterpret_cast<const f32x4*>(e.bias + n_base + 32 * jp + 8 * fg + 4 * h);
-      if (e.lnstat)
+      if constexpr (LNF)
         cs[jp][h] = *reinterpret_cast<const f32x4*>(e.colsum + n_base + 32 * jp + 8 * fg + 4 * h);
     }
 #pragma unroll
@@ -553,7 +556,7 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
         f32x4 v0 = acc[i0 + i][2 * jp];
         f32x4 v1 = acc[i0 + i][2 * jp + 1];
         const int mrow = m_base + 16 * (i0 + i) + fr, ncol = n_base + 32 * jp + 8 * fg;
-        if (e.lnstat)
+        if constexpr (LNF)
           epi_lnfold8(e, lst, mrow, 16 * (i0 + i) + fr, cs[jp][0], cs[jp][1], v0, v1);
         v0 += bias[jp][0];
         v1 += bias[jp][1];
@@ -569,7 +572,7 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
           const i32x4 o = {(int)pack_bf16x2(v0[0], v0[1]), (int)pack_bf16x2(v0[2], v0[3]),
                            (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
           store_out16(static_cast<bf16_t*>(e.out) + idx, o);
-          if (e.statout) {
+          if constexpr (STAT) {
             ob[jp] = o;
             tsum += bf16x8_sum(o);
           }
@@ -579,7 +582,7 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
           *reinterpret_cast<f32x4*>(op + 4) = v1;
         }
       }
-      if (OUT_BF16 && e.statout) {   // the row's 64 columns: lanes fr, fr + 16, + 32, + 48
+      if constexpr (OUT_BF16 && STAT) {   // the row's 64 columns: lanes fr, fr + 16, + 32, + 48
         // block mean (lane-swap butterfly: every lane holds it), then the centred sum of
         // squares of the same stored values
         const float mean = xsum32(xsum16(tsum)) * (1.f / 64.f);
@@ -644,7 +647,7 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
   // LayerNorm-fold row statistics of the wave's 128 rows: issued before the K loop (the
   // oldest vector-memory op, so the loop's counted waits retire it), used in the epilogue
   float2 lst[2] = {float2{0.f, 0.f}, float2{0.f, 0.f}};
-  if (e.lnstat) {
+  if constexpr (EPI != EPI_GENERIC && (EPI & EPI_LNF) != 0) {
     lst[0] = e.lnstat[min(m0 + wm * 128 + lane, M - 1)];
     lst[1] = e.lnstat[min(m0 + wm * 128 + 64 + lane, M - 1)];
   }
@@ -961,7 +964,10 @@ void pp2_set_attributes() {
     const void* fns[] = {VTD_PP_FN(EPI_GENERIC) VTD_PP_FN(0) VTD_PP_FN(1) VTD_PP_FN(2)
                          VTD_PP_FN(4) VTD_PP_FN(5) VTD_PP_FN(6) VTD_PP_FN(8) VTD_PP_FN(9)
                          VTD_PP_FN(10) VTD_PP_FN(12) VTD_PP_FN(13) VTD_PP_FN(14)
-                         VTD_PP_FN(EPI_PARTIAL)};
+                         VTD_PP_FN(EPI_PARTIAL) VTD_PP_FN(4 | EPI_LNF) VTD_PP_FN(5 | EPI_LNF)
+                         VTD_PP_FN(6 | EPI_LNF) VTD_PP_FN(4 | EPI_STAT) VTD_PP_FN(5 | EPI_STAT)
+                         VTD_PP_FN(6 | EPI_STAT) VTD_PP_FN(12 | EPI_STAT)
+                         VTD_PP_FN(13 | EPI_STAT) VTD_PP_FN(14 | EPI_STAT)};
 #undef VTD_PP_FN
     for (const void* f : fns)
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
@@ -1050,7 +1056,10 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
     EpiArgs e = make_epi_args(epi);
     e.ngw = ngw;
     const bool fast = pp2_fast_epilogue(epi);
-    const int code = fast ? epi_code(e.act, e.out_dtype == VTD_BF16, e.resid != nullptr)
+    // the fold / statistics bits select their specialised epilogues; a combination without
+    // one (e.g. a fold with a residual) takes the generic epilogue, which reads both at run time
+    const int code = fast ? epi_code(e.act, e.out_dtype == VTD_BF16, e.resid != nullptr) |
+                                (e.lnstat ? EPI_LNF : 0) | (e.statout ? EPI_STAT : 0)
                           : EPI_GENERIC;
     // transposed accumulators + register-direct epilogue for activation layers (mlp1 -5 %,
     // mlp2 -1.5 %), LDS-staged row vectors for the others (attn_out -10 %, mlp3 -4 %)
@@ -1061,6 +1070,9 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
   case C: pp2_launch<C>(tr, g, stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e); break;
       VTD_PP_CASE(0) VTD_PP_CASE(1) VTD_PP_CASE(2) VTD_PP_CASE(4) VTD_PP_CASE(5) VTD_PP_CASE(6)
       VTD_PP_CASE(8) VTD_PP_CASE(9) VTD_PP_CASE(10) VTD_PP_CASE(12) VTD_PP_CASE(13) VTD_PP_CASE(14)
+      VTD_PP_CASE(4 | EPI_LNF) VTD_PP_CASE(5 | EPI_LNF) VTD_PP_CASE(6 | EPI_LNF)
+      VTD_PP_CASE(4 | EPI_STAT) VTD_PP_CASE(5 | EPI_STAT) VTD_PP_CASE(6 | EPI_STAT)
+      VTD_PP_CASE(12 | EPI_STAT) VTD_PP_CASE(13 | EPI_STAT) VTD_PP_CASE(14 | EPI_STAT)
 #undef VTD_PP_CASE
       default:
         pp2_launch<EPI_GENERIC>(tr, g, stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);
@@ -1183,7 +1195,8 @@ int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_
 #define VTD_MX_FN(C) reinterpret_cast<const void*>(&gemm_mx8_pp_kernel<C>),
     const void* fns[] = {VTD_MX_FN(EPI_GENERIC) VTD_MX_FN(0) VTD_MX_FN(1) VTD_MX_FN(2)
                          VTD_MX_FN(4) VTD_MX_FN(5) VTD_MX_FN(6) VTD_MX_FN(8) VTD_MX_FN(9)
-                         VTD_MX_FN(10) VTD_MX_FN(12) VTD_MX_FN(13) VTD_MX_FN(14)};
+                         VTD_MX_FN(10) VTD_MX_FN(12) VTD_MX_FN(13) VTD_MX_FN(14)
+                         VTD_MX_FN(4 | EPI_F8O) VTD_MX_FN(5 | EPI_F8O) VTD_MX_FN(6 | EPI_F8O)};
 #undef VTD_MX_FN
     for (const void* f : fns)
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * MXP_STAGE);
@@ -1193,7 +1206,8 @@ int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_
                     reinterpret_cast<uintptr_t>(e.out) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(e.bias) % 16 == 0 &&
                     (!e.resid || reinterpret_cast<uintptr_t>(e.resid) % 16 == 0);
-  const int code = fast ? epi_code(e.act, e.out_dtype != VTD_F32, e.resid != nullptr)
+  const int code = fast ? epi_code(e.act, e.out_dtype != VTD_F32, e.resid != nullptr) |
+                              (e.out_dtype == VTD_FP8 ? EPI_F8O : 0)
                         : EPI_GENERIC;
   const dim3 g(tiles_m * tiles_n), b(BNT);
   switch (code) {
@@ -1204,7 +1218,8 @@ int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_
     break;
     VTD_MX_CASE(0) VTD_MX_CASE(1) VTD_MX_CASE(2) VTD_MX_CASE(4) VTD_MX_CASE(5)
     VTD_MX_CASE(6) VTD_MX_CASE(8) VTD_MX_CASE(9) VTD_MX_CASE(10) VTD_MX_CASE(12)
-    VTD_MX_CASE(13) VTD_MX_CASE(14)
+    VTD_MX_CASE(13) VTD_MX_CASE(14) VTD_MX_CASE(4 | EPI_F8O) VTD_MX_CASE(5 | EPI_F8O)
+    VTD_MX_CASE(6 | EPI_F8O)
 #undef VTD_MX_CASE
     default:
       hipLaunchKernelGGL((gemm_mx8_pp_kernel<EPI_GENERIC>), g, b, 2 * MXP_STAGE, stream, M, N, K,

@@ -221,6 +221,10 @@ __device__ __forceinline__ void epi_store4(const EpiArgs& e, int M, int N, int m
 constexpr int EPI_GENERIC = -1;
 // pp2 split-K partial launches: fp32 raw sums, no bias / activation / residual (vtd_gemm.hip)
 constexpr int EPI_PARTIAL = 16;
+// compile-time epilogue modes of the fast (pp2 / MX ping-pong) epilogues: the LayerNorm fold
+// (epilogue.lnstat / colsum), the partial row statistics (epilogue.statout) and the MX-fp8
+// output (out_dtype VTD_FP8) -- per-row uniform branches gone from the unrolled store loops
+constexpr int EPI_LNF = 32, EPI_STAT = 64, EPI_F8O = 128;
 __host__ __device__ constexpr int epi_code(int act, bool out_bf16, bool resid) {
   return act | (out_bf16 ? 4 : 0) | (resid ? 8 : 0);
 }
