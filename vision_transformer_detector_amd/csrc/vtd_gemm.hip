@@ -214,13 +214,13 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
       if constexpr (LNF) epi_lnfold8(e, lst, m_base + p * PR + row, p * PR + row, cs0, cs1, v0, v1);
       v0 += b0;
       v1 += b1;
-      if (e.rowadd) epi_rowadd8(e, m_base + p * PR + row, n_base + c8, v0, v1);
+      if constexpr ((EPI & EPI_RA) != 0) epi_rowadd8(e, m_base + p * PR + row, n_base + c8, v0, v1);
       act_ct8<ACT>(v0, v1);
       if constexpr (RESID) {
         v0 += rv[it][0];
         v1 += rv[it][1];
       }
-      if (e.out2) epi_out2_8(e, m_base + p * PR + row, n_base + c8, v0, v1);
+      if constexpr ((EPI & EPI_O2) != 0) epi_out2_8(e, m_base + p * PR + row, n_base + c8, v0, v1);
       const int64_t idx = (int64_t)(m_base + p * PR + row) * e.ldo + n_base + c8;
       if constexpr (OUT_BF16) {
         if constexpr (F8O) {
@@ -560,13 +560,13 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
           epi_lnfold8(e, lst, mrow, 16 * (i0 + i) + fr, cs[jp][0], cs[jp][1], v0, v1);
         v0 += bias[jp][0];
         v1 += bias[jp][1];
-        if (e.rowadd) epi_rowadd8(e, mrow, ncol, v0, v1);
+        if constexpr ((EPI & EPI_RA) != 0) epi_rowadd8(e, mrow, ncol, v0, v1);
         act_ct8<ACT>(v0, v1);
         if constexpr (RESID) {
           v0 += rv[i][jp][0];
           v1 += rv[i][jp][1];
         }
-        if (e.out2) epi_out2_8(e, mrow, ncol, v0, v1);
+        if constexpr ((EPI & EPI_O2) != 0) epi_out2_8(e, mrow, ncol, v0, v1);
         const int64_t idx = (int64_t)mrow * e.ldo + ncol;
         if constexpr (OUT_BF16) {
           const i32x4 o = {(int)pack_bf16x2(v0[0], v0[1]), (int)pack_bf16x2(v0[2], v0[3]),
@@ -967,7 +967,8 @@ void pp2_set_attributes() {
                          VTD_PP_FN(EPI_PARTIAL) VTD_PP_FN(4 | EPI_LNF) VTD_PP_FN(5 | EPI_LNF)
                          VTD_PP_FN(6 | EPI_LNF) VTD_PP_FN(4 | EPI_STAT) VTD_PP_FN(5 | EPI_STAT)
                          VTD_PP_FN(6 | EPI_STAT) VTD_PP_FN(12 | EPI_STAT)
-                         VTD_PP_FN(13 | EPI_STAT) VTD_PP_FN(14 | EPI_STAT)};
+                         VTD_PP_FN(13 | EPI_STAT) VTD_PP_FN(14 | EPI_STAT)
+                         VTD_PP_FN(4 | EPI_STAT | EPI_RA) VTD_PP_FN(4 | EPI_RA)};
 #undef VTD_PP_FN
     for (const void* f : fns)
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
@@ -1059,7 +1060,8 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
     // the fold / statistics bits select their specialised epilogues; a combination without
     // one (e.g. a fold with a residual) takes the generic epilogue, which reads both at run time
     const int code = fast ? epi_code(e.act, e.out_dtype == VTD_BF16, e.resid != nullptr) |
-                                (e.lnstat ? EPI_LNF : 0) | (e.statout ? EPI_STAT : 0)
+                                (e.lnstat ? EPI_LNF : 0) | (e.statout ? EPI_STAT : 0) |
+                                (e.rowadd ? EPI_RA : 0) | (e.out2 ? EPI_O2 : 0)
                           : EPI_GENERIC;
     // transposed accumulators + register-direct epilogue for activation layers (mlp1 -5 %,
     // mlp2 -1.5 %), LDS-staged row vectors for the others (attn_out -10 %, mlp3 -4 %)
@@ -1073,6 +1075,7 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
       VTD_PP_CASE(4 | EPI_LNF) VTD_PP_CASE(5 | EPI_LNF) VTD_PP_CASE(6 | EPI_LNF)
       VTD_PP_CASE(4 | EPI_STAT) VTD_PP_CASE(5 | EPI_STAT) VTD_PP_CASE(6 | EPI_STAT)
       VTD_PP_CASE(12 | EPI_STAT) VTD_PP_CASE(13 | EPI_STAT) VTD_PP_CASE(14 | EPI_STAT)
+      VTD_PP_CASE(4 | EPI_STAT | EPI_RA) VTD_PP_CASE(4 | EPI_RA)
 #undef VTD_PP_CASE
       default:
         pp2_launch<EPI_GENERIC>(tr, g, stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);

@@ -225,6 +225,9 @@ constexpr int EPI_PARTIAL = 16;
 // (epilogue.lnstat / colsum), the partial row statistics (epilogue.statout) and the MX-fp8
 // output (out_dtype VTD_FP8) -- per-row uniform branches gone from the unrolled store loops
 constexpr int EPI_LNF = 32, EPI_STAT = 64, EPI_F8O = 128;
+// and the rare runtime modes: the position-embedding row add (patch embedding) and the bf16
+// copy of an f32 residual stream (out2)
+constexpr int EPI_RA = 256, EPI_O2 = 512;
 __host__ __device__ constexpr int epi_code(int act, bool out_bf16, bool resid) {
   return act | (out_bf16 ? 4 : 0) | (resid ? 8 : 0);
 }
