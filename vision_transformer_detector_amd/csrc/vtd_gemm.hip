@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <type_traits>
 
 #include "vtd_common.h"
 #include "vtd_gemm_epi.h"
@@ -467,15 +468,17 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
   if (wm == 1) pp_barrier();                 // stagger G1 by one barrier
   const int ra = wm * 64, rb = wn * 32;      // group rows of this wave's quads
   bf16x8 a[4][2], b0[2][2], b1[2][2];
-  for (int kt = 0; kt < nk; ++kt) {
+  // one K-step; n1 / n2 = K-tiles kt + 1 / kt + 2 exist.  The steady-state steps (both) and the
+  // last two are separate compile-time bodies: no per-phase branches in the main loop
+  auto step = [&](int kt, auto t1, auto t2) {
     const char* st = smem + (kt & 1) * BSTAGE;
-    const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+    constexpr bool n1 = decltype(t1)::value, n2 = decltype(t2)::value;
     // ---- P0
     pp_load_a(a, st + 0 * 16384, ra, fr, fg);
     if constexpr (TR) pp_load_b_t(b0, st + 2 * 16384, rb, fr, fg);
     else pp_load_b(b0, st + 2 * 16384, rb, fr, fg);
-    if (n1) pp2_issue<1>(smem, src, wave, kt + 1, (kt + 1) & 1);
-    if (n1) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    if constexpr (n1) pp2_issue<1>(smem, src, wave, kt + 1, (kt + 1) & 1);
+    if constexpr (n1) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     pp_barrier();
     if constexpr (TR) pp_mfma_t<0, 0>(acc, a, b0);
@@ -484,7 +487,7 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
     // ---- P1
     if constexpr (TR) pp_load_b_t(b1, st + 3 * 16384, rb, fr, fg);
     else pp_load_b(b1, st + 3 * 16384, rb, fr, fg);
-    if (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    if constexpr (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     pp_barrier();
     if constexpr (TR) pp_mfma_t<0, 2>(acc, a, b1);
@@ -492,13 +495,13 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
     pp_barrier();
     // ---- P2
     pp_load_a(a, st + 1 * 16384, ra, fr, fg);
-    if (n2) pp2_issue<0>(smem, src, wave, kt + 2, kt & 1);
+    if constexpr (n2) pp2_issue<0>(smem, src, wave, kt + 2, kt & 1);
     pp_barrier();
     if constexpr (TR) pp_mfma_t<4, 2>(acc, a, b1);
     else pp_mfma<4, 2>(acc, a, b1);
     pp_barrier();
     // ---- P3
-    if (n2) {
+    if constexpr (n2) {
       pp2_issue<2>(smem, src, wave, kt + 2, kt & 1);
       pp2_issue<3>(smem, src, wave, kt + 2, kt & 1);
       asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
@@ -509,7 +512,11 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
     if constexpr (TR) pp_mfma_t<4, 0>(acc, a, b0);
     else pp_mfma<4, 0>(acc, a, b0);
     pp_barrier();
-  }
+  };
+  int kt = 0;
+  for (; kt + 2 < nk; ++kt) step(kt, std::true_type{}, std::true_type{});
+  if (kt + 1 < nk) step(kt++, std::true_type{}, std::false_type{});
+  step(kt, std::false_type{}, std::false_type{});
   if (wm == 0) pp_barrier();                 // re-align
 }
 
@@ -821,9 +828,10 @@ __global__ __launch_bounds__(BNT) void gemm_mx8_pp_kernel(
   const int sa_row = wm * 128 + fr, sb_row = wn * 64 + fr;
   bf16x8 a[4][2], b0[2][2], b1[2][2];
   int sa[8], sb[4];
-  for (int kt = 0; kt < nk; ++kt) {
+  // one K-step, the last two peeled at compile time (as pp2_mainloop)
+  auto step = [&](int kt, auto t1, auto t2) {
     const char* st = smem + (kt & 1) * MXP_STAGE;
-    const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+    constexpr bool n1 = decltype(t1)::value, n2 = decltype(t2)::value;
     // ---- P0 (also every scale of the tile: X0 / Y0 refill them two tiles ahead)
     pp_load_a(a, st + 0 * 16384, ra, fr, fg);
     pp_load_b(b0, st + 2 * 16384, rb, fr, fg);
@@ -833,27 +841,27 @@ __global__ __launch_bounds__(BNT) void gemm_mx8_pp_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       sb[j] = *reinterpret_cast<const int*>(st + BSTAGE + 1024 + (sb_row + 16 * j) * 4) >> (8 * fg);
-    if (n1) mxp_issue<1>(smem, src, wave, lane, kt + 1, (kt + 1) & 1);
-    if (n1) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    if constexpr (n1) mxp_issue<1>(smem, src, wave, lane, kt + 1, (kt + 1) & 1);
+    if constexpr (n1) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     pp_barrier();
     mxp_mfma<0, 0>(acc, a, b0, sa, sb);
     pp_barrier();
     // ---- P1
     pp_load_b(b1, st + 3 * 16384, rb, fr, fg);
-    if (n1) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    if constexpr (n1) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     pp_barrier();
     mxp_mfma<0, 2>(acc, a, b1, sa, sb);
     pp_barrier();
     // ---- P2
     pp_load_a(a, st + 1 * 16384, ra, fr, fg);
-    if (n2) mxp_issue<0>(smem, src, wave, lane, kt + 2, kt & 1);
+    if constexpr (n2) mxp_issue<0>(smem, src, wave, lane, kt + 2, kt & 1);
     pp_barrier();
     mxp_mfma<4, 2>(acc, a, b1, sa, sb);
     pp_barrier();
     // ---- P3
-    if (n2) {
+    if constexpr (n2) {
       mxp_issue<2>(smem, src, wave, lane, kt + 2, kt & 1);
       mxp_issue<3>(smem, src, wave, lane, kt + 2, kt & 1);
       asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
@@ -863,7 +871,11 @@ __global__ __launch_bounds__(BNT) void gemm_mx8_pp_kernel(
     pp_barrier();
     mxp_mfma<4, 0>(acc, a, b0, sa, sb);
     pp_barrier();
-  }
+  };
+  int kt = 0;
+  for (; kt + 2 < nk; ++kt) step(kt, std::true_type{}, std::true_type{});
+  if (kt + 1 < nk) step(kt++, std::true_type{}, std::false_type{});
+  step(kt, std::false_type{}, std::false_type{});
   if (wm == 0) pp_barrier();                 // re-align
   float* ep = reinterpret_cast<float*>(smem) + wave * 32 * 68;
   const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
