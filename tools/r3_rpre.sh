@@ -1,0 +1,21 @@
+#!/bin/bash
+# round 3: bf16 residual rows prefetched one pass ahead in the GEMM epilogues (libvtd.so) vs
+# HEAD (libvtd_base.so): GEMM tests + goldens, then interleaved forward A/B
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+mkdir -p $R/gpurun_out
+cd $R
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_kernels.py tests/test_gpu_mx8.py -m gpu -k "gemm or statout or fold or mx8 or resid" > gpurun_out/r3_rpre_tests.log 2>&1 || { tail -40 gpurun_out/r3_rpre_tests.log; exit 1; }
+tail -1 gpurun_out/r3_rpre_tests.log
+timeout -k 10 500 python -u -m pytest -x -q -s --timeout 300 --timeout-method thread tests/test_gpu_batch_parity.py tests/test_gpu_model.py -m gpu > gpurun_out/r3_rpre_parity.log 2>&1 || { tail -30 gpurun_out/r3_rpre_parity.log; exit 1; }
+grep -i 'max-rel' gpurun_out/r3_rpre_parity.log; tail -1 gpurun_out/r3_rpre_parity.log
+O=gpurun_out/r3_rpre.log
+run() {  # label, lib, bench args...
+  local lab=$1; shift; local lib=$1; shift
+  VTD_LIB_PATH=$R/vision_transformer_detector_amd/$lib.so timeout -k 10 300 python -u bench.py --no-cpu-baseline "$@" > /tmp/b.json 2>/dev/null || exit 1
+  python3 -c "import json;d=json.load(open('/tmp/b.json'));print('$lab', d['value'], d['mfma_util_attn_mlp'], d['roofline']['avg_launch_us'])" | tee -a $O
+}
+for r in 1 2 3; do
+  run c2_new libvtd --steps 20 --warmup 5
+  run c2_base libvtd_base --steps 20 --warmup 5
+done

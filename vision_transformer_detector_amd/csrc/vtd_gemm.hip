@@ -190,6 +190,20 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
     cs0 = *reinterpret_cast<const f32x4*>(e.colsum + n_base + c8);
     cs1 = *reinterpret_cast<const f32x4*>(e.colsum + n_base + c8 + 4);
   }
+  // bf16 residual stream: each pass's rows loaded as raw 16-B words one pass ahead (the rows
+  // of pass p + 1 are in flight while pass p is staged and stored; they are rows this wave
+  // alone writes, so the in-place update cannot overtake the prefetch)
+  constexpr bool RPRE = RESID && OUT_BF16;
+  i32x4 rraw[2][NIT];
+  auto load_raw = [&](int pp, i32x4 (&dst)[NIT]) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int64_t m = m_base + pp * PR + it * 8 + rsub;
+      dst[it] = *reinterpret_cast<const i32x4*>(static_cast<const bf16_t*>(e.resid) + m * e.ldr +
+                                                n_base + c8);
+    }
+  };
+  if constexpr (RPRE) load_raw(0, rraw[0]);
 #pragma unroll
   for (int p = 0; p < 128 / PR; ++p) {
 #pragma unroll
@@ -199,8 +213,11 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
 #pragma unroll
         for (int r2 = 0; r2 < 4; ++r2)
           ep[(i * 16 + fg * 4 + r2) * ES + j * 16 + fr] = acc[p * NB + i][j][r2];
+    if constexpr (RPRE) {
+      if (p + 1 < 128 / PR) load_raw(p + 1, rraw[(p + 1) & 1]);
+    }
     f32x4 rv[NIT][2];
-    if constexpr (RESID) {
+    if constexpr (RESID && !RPRE) {
 #pragma unroll
       for (int it = 0; it < NIT; ++it) {
         const int64_t m = m_base + p * PR + it * 8 + rsub;
@@ -217,7 +234,11 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
       v1 += b1;
       if constexpr ((EPI & EPI_RA) != 0) epi_rowadd8(e, m_base + p * PR + row, n_base + c8, v0, v1);
       act_ct8<ACT>(v0, v1);
-      if constexpr (RESID) {
+      if constexpr (RPRE) {
+        const i32x4 w = rraw[p & 1][it];
+        v0 += bf16x4_to_f32((uint32_t)w[0], (uint32_t)w[1]);
+        v1 += bf16x4_to_f32((uint32_t)w[2], (uint32_t)w[3]);
+      } else if constexpr (RESID) {
         v0 += rv[it][0];
         v1 += rv[it][1];
       }
@@ -542,10 +563,26 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
       if constexpr (LNF)
         cs[jp][h] = *reinterpret_cast<const f32x4*>(e.colsum + n_base + 32 * jp + 8 * fg + 4 * h);
     }
+  // bf16 residual: the second half's rows (raw 16-B words) are loaded while the first half
+  // is computed
+  constexpr bool RPRE = RESID && OUT_BF16;
+  i32x4 rraw[2][4][2];
+  auto load_raw = [&](int h0, i32x4 (&dst)[4][2]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp)
+        dst[i][jp] = *reinterpret_cast<const i32x4*>(
+            static_cast<const bf16_t*>(e.resid) + (int64_t)(m_base + 16 * (h0 + i) + fr) * e.ldr +
+            n_base + 32 * jp + 8 * fg);
+  };
+  if constexpr (RPRE) load_raw(0, rraw[0]);
 #pragma unroll
   for (int i0 = 0; i0 < 8; i0 += 4) {
     f32x4 rv[4][2][2];
-    if constexpr (RESID) {
+    if constexpr (RPRE) {
+      if (i0 == 0) load_raw(4, rraw[1]);
+    } else if constexpr (RESID) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -569,7 +606,11 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
         v1 += bias[jp][1];
         if constexpr ((EPI & EPI_RA) != 0) epi_rowadd8(e, mrow, ncol, v0, v1);
         act_ct8<ACT>(v0, v1);
-        if constexpr (RESID) {
+        if constexpr (RPRE) {
+          const i32x4 w = rraw[i0 >> 2][i][jp];
+          v0 += bf16x4_to_f32((uint32_t)w[0], (uint32_t)w[1]);
+          v1 += bf16x4_to_f32((uint32_t)w[2], (uint32_t)w[3]);
+        } else if constexpr (RESID) {
           v0 += rv[i][jp][0];
           v1 += rv[i][jp][1];
         }
