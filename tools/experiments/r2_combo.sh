@@ -1,4 +1,4 @@
 set -o pipefail
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
 tail -1 gpurun_out/gpu_tests.log
-bash tools/r2_ngw.sh
+bash tools/experiments/r2_ngw.sh
