@@ -61,6 +61,30 @@ static const uint8_t kJpeg[] = {
     157,40,65,168,104,210,118,245,87,234,158,218,253,231,255,217,
 };
 
+// 11x9 4:2:0 progressive JPEG (SOF2, libjpeg's simple progression script: 10 scans; Pillow,
+// quality 70, random pixels)
+static const uint8_t kJpegProg[] = {
+    255,216,255,224,0,16,74,70,73,70,0,1,1,0,0,1,0,1,0,0,255,219,0,67,0,10,7,7,8,7,6,10,8,8,8,11,10,
+    10,11,14,24,16,14,13,13,14,29,21,22,17,24,35,31,37,36,34,31,34,33,38,43,55,47,38,41,52,41,33,34,
+    48,65,49,52,57,59,62,62,62,37,46,68,73,67,60,72,55,61,62,59,255,219,0,67,1,10,11,11,14,13,14,28,
+    16,16,28,59,40,34,40,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,
+    59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,59,255,194,0,17,8,0,9,0,
+    11,3,1,34,0,2,17,1,3,17,1,255,196,0,23,0,0,3,1,0,0,0,0,0,0,0,0,0,0,0,0,0,1,2,3,4,255,196,0,21,1,
+    1,1,0,0,0,0,0,0,0,0,0,0,0,0,0,0,2,3,255,218,0,12,3,1,0,2,16,3,16,0,0,1,121,12,130,95,255,196,0,
+    25,16,1,1,0,3,1,0,0,0,0,0,0,0,0,0,0,0,1,2,3,4,50,52,255,218,0,8,1,1,0,1,5,2,100,36,207,112,87,
+    59,126,175,255,196,0,23,17,0,3,1,0,0,0,0,0,0,0,0,0,0,0,0,0,0,1,66,97,255,218,0,8,1,3,1,1,63,1,
+    149,167,255,196,0,23,17,0,3,1,0,0,0,0,0,0,0,0,0,0,0,0,0,0,2,17,1,255,218,0,8,1,2,1,1,63,1,93,
+    175,15,255,196,0,31,16,0,2,1,2,7,0,0,0,0,0,0,0,0,0,0,0,0,2,17,1,3,18,81,113,114,129,130,193,255,
+    218,0,8,1,1,0,6,63,2,196,171,57,82,57,33,109,214,55,157,95,194,230,167,255,196,0,29,16,0,2,2,1,
+    5,0,0,0,0,0,0,0,0,0,0,0,1,17,0,49,81,16,33,65,97,129,255,218,0,8,1,1,0,1,63,33,4,160,6,166,27,
+    140,46,123,129,135,213,132,66,253,148,233,3,255,218,0,12,3,1,0,2,0,3,0,0,0,16,15,255,196,0,25,
+    17,1,0,2,3,0,0,0,0,0,0,0,0,0,0,0,0,1,0,33,49,97,193,255,218,0,8,1,3,1,1,63,16,80,100,26,56,208,
+    246,231,255,196,0,27,17,0,1,4,3,0,0,0,0,0,0,0,0,0,0,0,0,1,0,17,65,113,33,49,81,255,218,0,8,1,2,
+    1,1,63,16,118,111,78,204,22,130,44,230,105,127,255,196,0,28,16,1,0,3,0,2,3,0,0,0,0,0,0,0,0,0,0,
+    1,0,17,33,97,240,49,65,81,255,218,0,8,1,1,0,1,63,16,101,25,7,133,75,116,52,182,202,226,172,97,
+    253,129,3,246,115,147,58,111,145,213,224,159,255,217,
+};
+
 int main() {
   CHECK(vtd_abi_version() == VTD_ABI_VERSION);
   // presets (presets.py): C1 reference default, C2 / C3 ViT-B/16, C5 ViT-L/16
@@ -152,6 +176,38 @@ int main() {
       f.insert(f.end(), seg, seg + 4);
       std::vector<uint8_t> exact(f.begin(), f.end());
       CHECK(vtd_jpeg_info(exact.data(), exact.size(), &h, &w, &c) != VTD_OK);
+    }
+  }
+  // progressive JPEG host side: per-scan table walk, planning of the scan / segment tables,
+  // every truncation (exactly sized copies) through both entry points, and a corrupted copy
+  {
+    int h = 0, w = 0, c = 0;
+    CHECK(vtd_jpeg_info(kJpegProg, sizeof(kJpegProg), &h, &w, &c) == VTD_OK);
+    CHECK(h == 9 && w == 11 && c == 3);
+    const uint8_t* ptrs[3] = {kJpegProg, kJpeg, kJpegProg};
+    size_t lens[3] = {sizeof(kJpegProg), sizeof(kJpeg), sizeof(kJpegProg)};
+    int32_t dims[6] = {0, 0, 0, 0, 0, 0};
+    size_t bytes = 0;
+    CHECK(vtd_jpeg_workspace_bytes(ptrs, lens, 3, dims, &bytes) == VTD_OK);
+    CHECK(dims[4] == 9 && dims[5] == 11 && bytes > 0);
+    for (size_t cut = 0; cut < sizeof(kJpegProg); ++cut) {
+      std::vector<uint8_t> part(kJpegProg, kJpegProg + cut);
+      (void)vtd_jpeg_info(part.data(), part.size(), &h, &w, &c);
+      const uint8_t* pp[1] = {part.data()};
+      size_t pl[1] = {part.size()};
+      int32_t pd[2];
+      size_t pb = 0;
+      (void)vtd_jpeg_workspace_bytes(pp, pl, 1, pd, &pb);
+    }
+    for (int stride : {3, 7, 13}) {
+      std::vector<uint8_t> bad(kJpegProg, kJpegProg + sizeof(kJpegProg));
+      for (size_t i = 2; i < bad.size(); i += stride) bad[i] ^= 0x5A;
+      (void)vtd_jpeg_info(bad.data(), bad.size(), &h, &w, &c);
+      const uint8_t* pp[1] = {bad.data()};
+      size_t pl[1] = {bad.size()};
+      int32_t pd[2];
+      size_t pb = 0;
+      (void)vtd_jpeg_workspace_bytes(pp, pl, 1, pd, &pb);
     }
   }
   // profiling state (host only)
