@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define VTD_ABI_VERSION 12
+#define VTD_ABI_VERSION 13
 #define VTD_KALIGN 64          /* K / row padding granule, elements              */
 #define VTD_MAX_MLP 16         /* max encoder_mlp_quantities                     */
 #define VTD_MAX_HEAD 64        /* max mlp_head layers * repeats                   */
@@ -56,8 +56,9 @@ typedef enum vtd_act {         /* activation fused in a GEMM epilogue           
   VTD_ACT_MISH = 2             /* MishActivation vtd.py:119-129                  */
 } vtd_act;
 
-/* create_vision_transformer_detector(...) kwargs, vtd.py:498-506.  dropout must be
- * None/0 (inference), max_weight/clip_weight only act on training (no-ops here). */
+/* create_vision_transformer_detector(...) kwargs, vtd.py:498-506.  dropout,
+ * max_weight and clip_weight only act on training (Keras Dropout / MHA dropout are the
+ * identity at inference; constraints apply after optimizer steps): no fields here. */
 typedef struct vtd_config {
   int batch;
   int image_h, image_w, channels;     /* input_shape                              */
@@ -302,10 +303,11 @@ int vtd_resize_with_pad(const uint8_t* pixels_dev, const int64_t* offsets_dev,
                         float* out_dev, void* stream);
 
 /* JPEG decode on the device, tf.image.decode_image(file, channels=3)
- * (vision_transformer_utilities.py:431) for baseline JPEG: sequential Huffman, 8-bit, 1 or 3
- * components, 4:4:4 / 4:2:2 / 4:2:0, restart intervals.  libjpeg-turbo's decode path (what TF
- * uses): ISLOW IDCT, fancy upsampling, YCbCr -> RGB; gray -> RGB replicated.  Other JPEGs
- * (progressive, CMYK, 12-bit, ...) return VTD_ERR_UNSUPPORTED with the reason.
+ * (vision_transformer_utilities.py:431) for baseline / extended sequential and progressive
+ * Huffman JPEG: 8-bit, 1 or 3 components, 4:4:4 / 4:2:2 / 4:2:0, restart intervals.
+ * libjpeg-turbo's decode path (what TF uses): ISLOW IDCT, fancy upsampling, YCbCr -> RGB;
+ * gray -> RGB replicated.  Other JPEGs (arithmetic-coded, lossless, 12-bit, 4:4:0, ...)
+ * return VTD_ERR_UNSUPPORTED with the reason.
  * vtd_jpeg_info: header only (host).  The images are HOST buffers; their marker segments are
  * parsed on the host, the entropy-coded data + derived tables copied to the workspace on
  * `stream` (through a pinned staging buffer the library reuses), image i written as RGB
@@ -365,6 +367,28 @@ int vtd_map_result(const float* latest_positive_bboxes, const float* labels_quan
 int vtd_profile_enable(int enable);
 int vtd_profile_reset(void);
 int vtd_profile_read(double* ms, int64_t* launches, double* flops, int n_classes);
+
+/* Run-time switches (kernel-variant A/B knobs).  Each is read ONCE per process from its
+ * environment variable at the first use of any knob; vtd_set_knob overrides one for the
+ * rest of the process (returns the previous value) so tests compare variants in one
+ * process.  -1 = unset: the library's default.
+ *   VTD_KNOB_ATTN_VARIANT (VTD_ATTN_VARIANT): bf16 attention kernel, 4 = persistent short-
+ *     sequence kernel where it applies (default), 2 = streaming, 3 = streaming 8-wave,
+ *     1 = the register-staged first kernel.
+ *   VTD_KNOB_ATTN_GRID (VTD_ATTN_GRID): persistent attention workgroups (default: CUs).
+ *   VTD_KNOB_GEMM_NGW (VTD_GEMM_NGW): GEMM tile-order group width (0 = row-major).
+ *   VTD_KNOB_SPLITK (VTD_SPLITK): 0 disables the head's split-K (changes workspace size).
+ *   VTD_KNOB_JPEG_CHUNK_BITS (VTD_JPEG_CHUNK_BITS): Huffman chunk length of vtd_jpeg_decode. */
+enum {
+  VTD_KNOB_ATTN_VARIANT = 0,
+  VTD_KNOB_ATTN_GRID = 1,
+  VTD_KNOB_GEMM_NGW = 2,
+  VTD_KNOB_SPLITK = 3,
+  VTD_KNOB_JPEG_CHUNK_BITS = 4,
+  VTD_KNOB_COUNT = 5
+};
+int vtd_set_knob(int knob, int value);
+int vtd_get_knob(int knob);
 
 #ifdef __cplusplus
 }

@@ -70,15 +70,15 @@ def test_jpeg_decode_bit_exact_vs_libjpeg_turbo(cuda, monkeypatch, chunk_bits):
     """chunk_bits: the smallest entropy-decode chunk (default 1024 bits); 64 cuts even the
     small images into many chunks, so nearly every chunk starts at a guessed decoder state
     and must resynchronise."""
+    from vision_transformer_detector_amd import _lib as L
     from vision_transformer_detector_amd.preprocess import decode_jpegs
-    if chunk_bits:
-        monkeypatch.setenv("VTD_JPEG_CHUNK_BITS", chunk_bits)
     files = [_encode(_image(h, w, i), mode, **kw) for i, (h, w, mode, kw) in enumerate(CASES)]
     for rst in (_restart_case(), _restart_case(720, 960, 1)):   # the second spans chunks
         if rst is not None:
             files.append(rst)
-    pixels, offsets, sizes = decode_jpegs(files, device=cuda)
-    torch.cuda.synchronize()
+    with L.knob(L.KNOB_JPEG_CHUNK_BITS, int(chunk_bits) if chunk_bits else -1):
+        pixels, offsets, sizes = decode_jpegs(files, device=cuda)
+        torch.cuda.synchronize()
     got = pixels.cpu().numpy()
     for i, f in enumerate(files):
         ref = _pil_rgb(f)

@@ -219,7 +219,7 @@ def test_attention(L, cuda, dtype, B, N, H, dk):
 
 @pytest.mark.parametrize("B,N,H", [(256, 196, 12), (5, 129, 7), (3, 224, 4), (1, 161, 1)])
 def test_attention_persistent_equals_per_pair_kernel(L, cuda, monkeypatch, B, N, H):
-    """The persistent short-sequence kernel (VTD_ATTN_VARIANT 4, the default for dkp 64 and
+    """The persistent short-sequence kernel (knob VTD_KNOB_ATTN_VARIANT 4, the default for dkp 64 and
     128 < N <= 256) against the per-(image, head) kernel, at the C2 shape (3072 pairs, 12 per
     workgroup) and ragged ones.  Its softmax takes the row's true max in one pass (all keys
     are in LDS) where the streaming kernel keeps a deferred running max, so P rounds to bf16
@@ -230,11 +230,11 @@ def test_attention_persistent_equals_per_pair_kernel(L, cuda, monkeypatch, B, N,
     g = torch.Generator().manual_seed(N + H)
     qkv = (torch.randn(B * N, ld, generator=g) * 1.5).to(torch.bfloat16).to(cuda)
     outs = []
-    for variant in ("2", "4"):
-        monkeypatch.setenv("VTD_ATTN_VARIANT", variant)
+    for variant in (2, 4):
         o = torch.full((B * N, H * dkp + 16), float("nan"), dtype=torch.bfloat16, device=cuda)
-        L.check(L.lib.vtd_attention(qkv.data_ptr(), B, N, H, dkp, ld, 0.125, o.data_ptr(),
-                                    H * dkp + 16, L.BF16, L.stream_ptr()), "attention")
+        with L.knob(L.KNOB_ATTN_VARIANT, variant):
+            L.check(L.lib.vtd_attention(qkv.data_ptr(), B, N, H, dkp, ld, 0.125, o.data_ptr(),
+                                        H * dkp + 16, L.BF16, L.stream_ptr()), "attention")
         torch.cuda.synchronize()
         outs.append(o.cpu())
     a, b = outs[0][:, :H * dkp].float(), outs[1][:, :H * dkp].float()
@@ -311,8 +311,8 @@ def test_bad_args_raise_value_error(L, cuda):
     (5000, 2304, 128, 0, 1), (3000, 1544, 3072, 1, 1), (6400, 2304, 2048, 0, 1),
     (2100, 512, 4096, 2, 1)])
 def test_gemm_bf16_256_tile_path(L, cuda, M, N, K, act, out_dtype):
-    """Large problems (>= 128 tiles of 256 x 256) take the DMA-staged 256-tile kernel (w4,
-    vtd_gemm_w4.hip); ragged M / N exercise the clamped loads and the masked epilogue."""
+    """Large problems (>= 128 tiles of 256 x 256) take the DMA-staged 256-tile kernel (pp2,
+    vtd_gemm.hip); ragged M / N exercise the clamped loads and the masked epilogue."""
     g = torch.Generator(device=cuda).manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
     Bt = (torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
@@ -344,17 +344,18 @@ def test_gemm_bf16_256_tile_path(L, cuda, M, N, K, act, out_dtype):
     (4096, 2048, 64, 1, False),      # one K-step (no steady-state loop)
     (4096, 2048, 128, 0, False)])    # two K-steps
 def test_gemm_variants_w4_pp2(L, cuda, monkeypatch, M, N, K, act, resid):
-    """The two 256-tile bf16 kernels (VTD_GEMM_VARIANT 10 = pp2, 8-wave ping-pong, the
-    default; 12 = w4, one wave per SIMD, persistent; VTD_W4_SCHED 1 / 2) against fp64 and
-    against each other (same K order of the fp32 accumulation: within bf16 output rounding),
-    with an in-place residual."""
+    """The 256-tile bf16 kernel (pp2, 8-wave ping-pong) against fp64 with an in-place
+    residual; with the diagnostic library (`make diag`, VTD_LIB_PATH) also the w4 kernel
+    (VTD_GEMM_VARIANT 12, one wave per SIMD, persistent; VTD_W4_SCHED 1 / 2) against fp64 and
+    against pp2 (same K order of the fp32 accumulation: within bf16 output rounding)."""
+    variants = ("10", "12", "12s2") if hasattr(L.lib, "vtd_diag_build") else ("10",)
     g = torch.Generator(device=cuda).manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
     Bt = (torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
     bias = torch.randn(N, generator=g, device=cuda)
     x0 = (4 * torch.randn(M, N, generator=g, device=cuda)).to(torch.bfloat16)
     outs = {}
-    for v in ("10", "12", "12s2"):
+    for v in variants:
         monkeypatch.setenv("VTD_GEMM_VARIANT", v[:2])
         monkeypatch.setenv("VTD_W4_SCHED", "2" if v.endswith("s2") else "1")
         x = x0.clone()
@@ -364,10 +365,12 @@ def test_gemm_variants_w4_pp2(L, cuda, monkeypatch, M, N, K, act, resid):
     ref64 = _np_act(act, (A.double() @ Bt.double().T + bias.double()).cpu().numpy())
     if resid:
         ref64 = ref64 + x0.double().cpu().numpy()
-    for v in ("10", "12", "12s2"):
+    for v in variants:
         got = outs[v].double().cpu().numpy()
         err = np.abs(got - ref64) / np.maximum(np.abs(ref64), 1.0)
         assert err.max() < 8e-3, (v, err.max(), np.argwhere(err >= 8e-3)[:5].tolist())
+    if len(variants) == 1:
+        return
     d = (outs["12"].float() - outs["10"].float()).abs() / outs["10"].float().abs().clamp(min=1.0)
     assert d.max().item() < 1.6e-2        # <= 2 bf16 ulps
     assert torch.equal(outs["12"], outs["12s2"])     # the schedules differ in timing only
@@ -375,7 +378,10 @@ def test_gemm_variants_w4_pp2(L, cuda, monkeypatch, M, N, K, act, resid):
 
 @pytest.mark.parametrize("variant", ["10", "12", "12s2"])
 def test_gemm_statout_variants(L, cuda, monkeypatch, variant):
-    """The producer-side LayerNorm partial statistics on both 256-tile kernels."""
+    """The producer-side LayerNorm partial statistics on the 256-tile kernels (w4: the
+    diagnostic library only)."""
+    if variant != "10" and not hasattr(L.lib, "vtd_diag_build"):
+        pytest.skip("the w4 kernel is in the diagnostic build only (make diag)")
     monkeypatch.setenv("VTD_GEMM_VARIANT", variant[:2])
     monkeypatch.setenv("VTD_W4_SCHED", "2" if variant.endswith("s2") else "1")
     M, N, K = 50176, 768, 768
@@ -684,3 +690,34 @@ def test_gemm_splitk_choice_and_args(L, cuda):
         with pytest.raises(ValueError):
             L.check(L.lib.vtd_gemm_splitk(64, 64, K, 1, K, 1, K, ctypes.byref(e), 1, nbytes, ks,
                                           L.stream_ptr()), "gemm_splitk")
+
+
+def test_gemm_statout_needs_a_specialised_epilogue(L, cuda):
+    """Partial LayerNorm statistics are written only by the specialised 256-tile epilogues:
+    a combination without one (the fold + residual + statistics of a single-layer MLP) is
+    refused with VTD_ERR_UNSUPPORTED instead of returning OK with the statistics unwritten
+    (ADVICE r3); the same GEMM without the fold still emits them."""
+    M, N, K = 32768, 512, 512
+    g = torch.Generator(device=cuda).manual_seed(3)
+    A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
+    Bt = (torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g, device=cuda)
+    colsum = Bt.float().sum(1).contiguous()
+    lnstat = torch.stack([A.float().mean(1), torch.ones(M, device=cuda)], 1).contiguous()
+    x = torch.randn(M, N, generator=g, device=cuda).to(torch.bfloat16)
+    stat = torch.full((M, N // 64, 2), float("nan"), device=cuda)
+    e = L.VtdEpilogue()
+    e.bias, e.act, e.out, e.ldo, e.out_dtype = bias.data_ptr(), L.ACT_GELU_TANH, x.data_ptr(), N, 1
+    e.resid, e.ldr = x.data_ptr(), N
+    e.lnstat, e.colsum = lnstat.data_ptr(), colsum.data_ptr()
+    e.statout, e.stat_ld = stat.data_ptr(), N // 64
+    rc = L.lib.vtd_gemm(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, L.BF16, ctypes.byref(e),
+                        L.stream_ptr())
+    assert rc == -2, (rc, L.lib.vtd_last_error())
+    e.lnstat, e.colsum = None, None
+    L.check(L.lib.vtd_gemm(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, L.BF16, ctypes.byref(e),
+                           L.stream_ptr()), "vtd_gemm")
+    torch.cuda.synchronize()
+    assert torch.isfinite(stat).all()
+    blocks = x.float().view(M, N // 64, 64)
+    assert torch.allclose(stat[..., 0], blocks.mean(-1), rtol=1e-5, atol=1e-5)

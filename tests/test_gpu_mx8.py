@@ -22,6 +22,12 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
+
+def _need_variant(L, variant):
+    """VTD_MX_VARIANT 2 / 3 (the x4 kernel) exist in the diagnostic library only."""
+    if variant != "1" and not hasattr(L.lib, "vtd_diag_build"):
+        pytest.skip("the x4 kernel is in the diagnostic build only (make diag)")
+
 def L(cuda):
     from vision_transformer_detector_amd import _lib
     return _lib
@@ -71,6 +77,7 @@ def test_quantize_matches_oracle(L, cuda, rows, K, Kq, src):
 @pytest.mark.parametrize("variant", ["1", "2"])
 def test_gemm_mx8_matches_dequantized_fp64(L, cuda, monkeypatch, variant, M, N, K, act,
                                            out_dtype, resid):
+    _need_variant(L, variant)
     monkeypatch.setenv("VTD_MX_VARIANT", variant)
     g = torch.Generator(device=cuda).manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
@@ -139,6 +146,7 @@ def test_gemm_mx8_fp8_output_equals_quantized_bf16_output(L, cuda, monkeypatch, 
                                                           K, act):
     """out_dtype VTD_FP8 (the next MX GEMM's operand written by the epilogue) equals the bf16
     output of the same GEMM passed through vtd_quantize_mx8, byte for byte."""
+    _need_variant(L, variant)
     monkeypatch.setenv("VTD_MX_VARIANT", variant)
     g = torch.Generator(device=cuda).manual_seed(M + N + K + 7)
     A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
@@ -174,7 +182,8 @@ def test_gemm_mx8_fp8_output_equals_quantized_bf16_output(L, cuda, monkeypatch, 
 def test_gemm_mx8_x4_equals_pingpong(L, cuda, monkeypatch, M, N, K, act, resid):
     """The two MX kernels compute each output as the same sequence of 128-wide scaled MFMA
     K-steps accumulated in fp32 in K order (x4 with the operands swapped: D^T = B A^T), so
-    their outputs agree bit for bit."""
+    their outputs agree bit for bit (x4: the diagnostic library only)."""
+    _need_variant(L, "2")
     g = torch.Generator(device=cuda).manual_seed(M * 3 + N + K)
     A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
     W = torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)
@@ -203,9 +212,16 @@ def test_attention_mx8_equals_attention_then_quantize(L, cuda, monkeypatch, B, N
     """The attention kernel's MX-fp8 epilogue (the VTD_FP8 attention-output operand) writes
     exactly the bytes of vtd_attention (bf16 out) followed by vtd_quantize_mx8.  The MX
     epilogue rides on the streaming (per-(image, head)) kernel, so the bf16 reference is that
-    kernel too (VTD_ATTN_VARIANT 2: at N = 196 the default bf16 path is the persistent kernel,
+    kernel too (knob VTD_KNOB_ATTN_VARIANT 2: at N = 196 the default bf16 path is the persistent kernel,
     whose one-pass softmax rounds P differently)."""
-    monkeypatch.setenv("VTD_ATTN_VARIANT", "2")
+    prev = L.lib.vtd_set_knob(L.KNOB_ATTN_VARIANT, 2)
+    try:
+        _attention_mx8_case(L, cuda, B, N, H, dkp)
+    finally:
+        L.lib.vtd_set_knob(L.KNOB_ATTN_VARIANT, prev)
+
+
+def _attention_mx8_case(L, cuda, B, N, H, dkp):
     g = torch.Generator(device=cuda).manual_seed(B * N + H)
     ld = 3 * H * dkp
     qkv = (torch.randn(B * N, ld, generator=g, device=cuda) * 1.5).to(torch.bfloat16)

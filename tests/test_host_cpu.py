@@ -45,9 +45,29 @@ def test_removed_switches_are_not_read_by_the_library(L):
     read them (the GPU test checks the logits with them set)."""
     blob = open(L.lib._name, "rb").read()
     for name in (b"VTD_ATTN_DIAG", b"VTD_PP3_DIAG", b"VTD_LN_FUSE", b"VTD_W4_DG",
-                 b"VTD_DIAG_NOFIN", b"VTD_DIAG_NOATTN", b"VTD_DIAG_NOHEAD"):
+                 b"VTD_DIAG_NOFIN", b"VTD_DIAG_NOATTN", b"VTD_DIAG_NOHEAD",
+                 # round 4: w4 / x4 and their switches live in the diagnostic build only
+                 b"VTD_GEMM_VARIANT", b"VTD_MX_VARIANT", b"VTD_W4_SCHED", b"VTD_X4_SCHED"):
         assert name + b"\0" not in blob, name
-    assert b"VTD_GEMM_VARIANT\0" in blob   # the live A/B switch: 10 (default) or 12
+    assert b"gemm_tn_bf16_w4" not in blob and b"gemm_mx8_x4" not in blob
+    assert not hasattr(L.lib, "vtd_diag_build")
+    # the run-time knobs are read from the environment once per process (vtd_set_knob)
+    for name in (b"VTD_ATTN_VARIANT", b"VTD_ATTN_GRID", b"VTD_GEMM_NGW", b"VTD_SPLITK",
+                 b"VTD_JPEG_CHUNK_BITS"):
+        assert name + b"\0" in blob, name
+
+
+def test_knobs_set_get_and_restore(L):
+    """vtd_set_knob returns the previous value; out-of-range knobs are rejected."""
+    for k in range(L.KNOB_JPEG_CHUNK_BITS + 1):
+        prev = L.lib.vtd_get_knob(k)
+        assert L.lib.vtd_set_knob(k, 7) == prev
+        assert L.lib.vtd_get_knob(k) == 7
+        with L.knob(k, 3):
+            assert L.lib.vtd_get_knob(k) == 3
+        assert L.lib.vtd_get_knob(k) == 7
+        assert L.lib.vtd_set_knob(k, prev) == 7
+    assert L.lib.vtd_set_knob(99, 1) == -1 and L.lib.vtd_get_knob(-1) == -1
 
 
 def test_ctypes_struct_layout_matches_c(L):

@@ -1,8 +1,8 @@
-# GPU-box check: full -m gpu suite, the w4 GEMM variant's tests, one bench line (gpurun -- bash tools/gpu_full.sh)
+# GPU-box check: full -m gpu suite, one bench line (gpurun -- bash tools/gpu_full.sh)
 set -o pipefail
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
 tail -2 gpurun_out/gpu_tests.log
-VTD_GEMM_VARIANT=12 timeout -k 10 200 python -u -m pytest tests/test_gpu_kernels.py -x -q -k gemm --timeout 120 --timeout-method thread > gpurun_out/gpu_tests11.log 2>&1 || { tail -30 gpurun_out/gpu_tests11.log; exit 1; }
-tail -1 gpurun_out/gpu_tests11.log
+
+
 timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 || { tail -20 gpurun_out/bench.log; exit 1; }
 tail -1 gpurun_out/bench.log

@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must precede loading libvtd.so, see module doc)
 LIB_PATH = os.environ.get("VTD_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                           "libvtd.so")
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 KALIGN = 64
 MAX_MLP = 16
 MAX_HEAD = 64
@@ -25,6 +25,8 @@ PROF_CLASSES = 5
 MAP_CLASSES, MAP_LATEST, MAP_PER_IMAGE, MAP_MAX_BOXES = 80, 3, 14, 64
 
 F32, BF16, FP8 = 0, 1, 2
+# run-time A/B knobs (vtd_set_knob; -1 = the library default)
+KNOB_ATTN_VARIANT, KNOB_ATTN_GRID, KNOB_GEMM_NGW, KNOB_SPLITK, KNOB_JPEG_CHUNK_BITS = 0, 1, 2, 3, 4
 ACT_NONE, ACT_GELU_TANH, ACT_MISH = 0, 1, 2
 STATUS = {0: "VTD_OK", -1: "VTD_ERR_INVALID_ARG", -2: "VTD_ERR_UNSUPPORTED",
           -3: "VTD_ERR_HIP", -4: "VTD_ERR_WORKSPACE"}
@@ -131,6 +133,8 @@ SIGNATURES = {
     "vtd_map_result": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "vtd_forward": (c_int, [ctypes.POINTER(VtdConfig), ctypes.POINTER(VtdWeights), c_void_p,
                             c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "vtd_set_knob": (c_int, [c_int, c_int]),
+    "vtd_get_knob": (c_int, [c_int]),
     "vtd_profile_enable": (c_int, [c_int]),
     "vtd_profile_reset": (c_int, []),
     "vtd_profile_read": (c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(c_int64),
@@ -177,3 +181,19 @@ def stream_ptr(stream=None) -> int:
 
 def ptr(t) -> int | None:
     return None if t is None else int(t.data_ptr())
+
+
+class knob:
+    """Context manager: `with knob(KNOB_ATTN_VARIANT, 2): ...` sets a run-time knob of the
+    library (vtd_set_knob) and restores the previous value on exit."""
+
+    def __init__(self, k: int, value: int):
+        self.k, self.value, self.prev = k, int(value), None
+
+    def __enter__(self):
+        self.prev = lib.vtd_set_knob(self.k, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        lib.vtd_set_knob(self.k, self.prev)
+        return False

@@ -749,10 +749,10 @@ int launch_bf16_ps(const void* qkv, int B, int N, int heads, int ldqkv, float sc
   });
   const int ncu = device_cu_count();
   const int npairs = B * heads;
-  // workgroups: one per CU (VTD_ATTN_GRID overrides, read per call: A/B of co-running
-  // the two micro-batch streams' attention on disjoint halves of the chip)
-  const char* genv = getenv("VTD_ATTN_GRID");
-  const int grid = std::min(npairs, genv && atoi(genv) > 0 ? atoi(genv) : ncu);
+  // workgroups: one per CU (knob VTD_KNOB_ATTN_GRID overrides: A/B of co-running the two
+  // micro-batch streams' attention on disjoint halves of the chip)
+  const int kg = knob(VTD_KNOB_ATTN_GRID);
+  const int grid = std::min(npairs, kg > 0 ? kg : ncu);
   auto* kern = NR == 160 ? attention_bf16_ps_kernel<5>
                : NR == 192 ? attention_bf16_ps_kernel<6>
                : NR == 224 ? attention_bf16_ps_kernel<7>
@@ -825,9 +825,9 @@ int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqk
   ProfScope ps(stream, PROF_ATTN,
                flops > 0 ? flops : 4.0 * B * heads * (double)N * N * dkp);
   if (dtype == VTD_BF16) {
-    // read per call (tests A/B the variants in one process; 12 getenv per forward)
-    const char* venv = getenv("VTD_ATTN_VARIANT");
-    const int v1 = venv ? atoi(venv) : 4;
+    // knob VTD_KNOB_ATTN_VARIANT (environment read once per process; tests set it per call)
+    const int kv = knob(VTD_KNOB_ATTN_VARIANT);
+    const int v1 = kv >= 0 ? kv : 4;
     // 4 (default): the persistent kernel where it applies (dkp 64, 128 < N <= 256, whole
     // 128-B rows and 16-B aligned row pitches), else as 2
     if (v1 == 4 && dkp == 64 && N > 128 && N <= 256 && ldqkv % 8 == 0 && ldo % 8 == 0 &&

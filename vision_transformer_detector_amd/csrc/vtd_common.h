@@ -46,6 +46,10 @@ void once_per_device(std::once_flag (&flags)[kMaxDevices], F&& fn) {
   std::call_once(flags[current_device()], fn);
 }
 
+// run-time A/B knob (vtd_set_knob): the environment's value read once per process, or the
+// override; -1 = unset (vtd_runtime.hip)
+int knob(int k);
+
 // profiling hooks (vtd_profile.cpp); no-ops unless enabled
 enum ProfClass { PROF_GEMM = 0, PROF_ATTN = 1, PROF_LN = 2, PROF_PATCH = 3, PROF_OTHER = 4 };
 struct ProfScope {

@@ -157,9 +157,8 @@ typedef __attribute__((address_space(1))) const void gbl_void_t;
 // waves run as two groups offset by one barrier (G0 = waves 0-3, G1 = waves 4-7; each SIMD
 // holds one wave of each), so one group's MFMAs overlap the other's LDS reads and DMA.
 // Operands go HBM/L2 -> LDS by buffer_load_dwordx4 ... lds into four 16 KiB DMA groups
-// per 64 KiB stage (pp2_mainloop).  Superseded as the default by the one-wave-per-SIMD w4
-// kernel (vtd_gemm_w4.hip); kept for the MX-fp8 kernel's shared pieces and as the A/B
-// reference.
+// per 64 KiB stage (pp2_mainloop).  The default (and, in the product library, the only)
+// 256-tile bf16 kernel; the MX-fp8 ping-pong kernel below shares its pieces.
 // ============================================================================
 
 // Writes the wave's 128 x 64 accumulator tile: 4 passes of 32 rows staged through the
@@ -930,35 +929,28 @@ __global__ __launch_bounds__(BNT) void gemm_mx8_pp_kernel(
 }
 }  // namespace
 
+#ifndef VTD_DIAG
+#define VTD_DIAG 0
+#endif
+#if VTD_DIAG
+// Diagnostic build only (`make diag`, vtd_gemm_w4.hip): the one-wave-per-SIMD w4 (bf16) and
+// x4 (MX-fp8) kernels, measured slower than / equal to the ping-pong kernels in the forward
+// (profiles/r03_fwd_ab.log, r03_bench_c5_b128_fp8_mx3_s2.log) and therefore not in the product
+// library.  VTD_GEMM_VARIANT = 12 selects w4; VTD_MX_VARIANT = 2 selects x4, 3 x4 for K >= 2048.
 bool gemm_w4_launch(int M, int N, int K, const bf16_t* A, int lda, const bf16_t* Bt, int ldb,
                     const vtd_epilogue* epi, int ngw, hipStream_t stream);
 void gemm_mx8_x4_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_t* sA,
                         int64_t sa_rows, const uint8_t* Bt, int ldb, const uint8_t* sB,
                         int64_t sb_rows, const vtd_epilogue* epi, int ngw, hipStream_t stream);
-
-// The MX-fp8 kernel: 1 = the 8-wave ping-pong gemm_mx8_pp_kernel, 2 = x4 (vtd_gemm_w4.hip, one
-// wave per SIMD, persistent), 3 = x4 for K >= 2048 only.  VTD_MX_VARIANT (read per call) picks one; same products, same
-// epilogue arithmetic.
-constexpr int kDefaultMxVariant = 1;
 int mx_variant() {
   const char* v = getenv("VTD_MX_VARIANT");
-  const int x = v ? atoi(v) : kDefaultMxVariant;
-  return (x >= 1 && x <= 3) ? x : kDefaultMxVariant;
+  return v ? atoi(v) : 1;
 }
-
-// The bf16 256 x 256-tile kernel: 10 = pp2 (8-wave ping-pong, default), 12 = w4
-// (vtd_gemm_w4.hip, one wave per SIMD, persistent).  Both compute the same products with the
-// same epilogue arithmetic; VTD_GEMM_VARIANT (read per call, for A/B in one process) picks
-// one, any other value means the default.  Measured (C2 B = 256 forward, two interleaved
-// rounds on one box, profiles/r03_fwd_ab.log): pp2 18.60k img/s, w4 17.89k (one barrier per
-// K-step) / 18.06k (two); isolated, w4 leads on qkv / mlp1 / head2 / 8192^3 and trails on
-// the residual layers (profiles/r03_gemm_w4_vs_pp2.jsonl).
-constexpr int kDefaultVariant = 10;
 int gemm_variant() {
   const char* v = getenv("VTD_GEMM_VARIANT");
-  const int x = v ? atoi(v) : kDefaultVariant;
-  return (x == 10 || x == 12) ? x : kDefaultVariant;
+  return v ? atoi(v) : 10;
 }
+#endif
 
 // Fewest 256 x 256 tiles for which the bf16 path takes the 256-tile kernels (below: the
 // 128 x 128 gemm_tn_kernel; measured within noise from 1 to 128 tiles on the head's GEMMs).
@@ -968,21 +960,59 @@ constexpr int kMinBigTiles = 128;
 // an XCD's B panels in its L2 (measured per shape, round 2: qkv / mlp1 / head1 -3.3..-4 %,
 // mlp2 -1.7 %); narrower N stays row-major.  VTD_GEMM_NGW overrides (0 = row-major).
 int tile_group_width(int tiles_n) {
-  const char* v = getenv("VTD_GEMM_NGW");
-  return v ? atoi(v) : tiles_n >= 8 ? 4 : tiles_n == 6 ? 3 : 0;
+  const int k = knob(VTD_KNOB_GEMM_NGW);
+  return k >= 0 ? k : tiles_n >= 8 ? 4 : tiles_n == 6 ? 3 : 0;
+}
+
+// The epilogue codes pp2 has a specialised (compile-time) kernel for: the activation /
+// bf16 output / residual bits and the fold, statistics and row-add combinations the forward
+// uses.  Every other combination runs the generic epilogue, which applies the fold, the row
+// add and out2 at run time but does NOT write partial statistics (gemm_emits_stats).
+#define VTD_PP2_CODES(X)                                                                     \
+  X(0) X(1) X(2) X(4) X(5) X(6) X(8) X(9) X(10) X(12) X(13) X(14) X(EPI_PARTIAL)               \
+  X(4 | EPI_LNF) X(5 | EPI_LNF) X(6 | EPI_LNF) X(4 | EPI_STAT) X(5 | EPI_STAT)                \
+  X(6 | EPI_STAT) X(12 | EPI_STAT) X(13 | EPI_STAT) X(14 | EPI_STAT)                          \
+  X(4 | EPI_STAT | EPI_RA) X(4 | EPI_RA)
+
+constexpr bool pp2_specialised(int code) {
+#define VTD_PP_IS(C) code == (C) ||
+  return VTD_PP2_CODES(VTD_PP_IS) false;
+#undef VTD_PP_IS
+}
+
+// whether the pp2 kernel can take its fast (specialised) epilogues for this epilogue
+bool pp2_fast_epilogue(const vtd_epilogue* e) {
+  auto al16 = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
+  return e->bias && !e->detections && e->scatter_tokens <= 0 && e->ldo % 8 == 0 &&
+         (!e->resid || e->ldr % 8 == 0) && al16(e->out) && al16(e->bias) &&
+         (!e->resid || al16(e->resid)) && (!e->out2 || (e->ldo2 % 8 == 0 && al16(e->out2)));
+}
+
+// the pp2 epilogue code for this epilogue: its specialised kernel when one exists, else
+// EPI_GENERIC
+int pp2_code(const vtd_epilogue* e) {
+  if (!pp2_fast_epilogue(e)) return EPI_GENERIC;
+  const int code = epi_code(e->act, e->out_dtype == VTD_BF16, e->resid != nullptr) |
+                   (e->lnstat ? EPI_LNF : 0) | (e->statout ? EPI_STAT : 0) |
+                   (e->rowadd ? EPI_RA : 0) | (e->out2 ? EPI_O2 : 0);
+  return pp2_specialised(code) ? code : EPI_GENERIC;
 }
 
 // Whether vtd_gemm can emit the partial LayerNorm statistics (epilogue.statout) for this
-// problem: every tile full and on the 256-tile fast epilogues with a bf16 output.
+// problem: every tile full and on a specialised 256-tile epilogue with the statistics bit
+// (the generic epilogue does not write them; e.g. the fold + residual + statistics of a
+// single-layer MLP has no specialised kernel: its caller takes the row-statistics pass).
 bool gemm_emits_stats(int M, int N, int dtype, const vtd_epilogue* e) {
   const int tiles = ((M + BBM - 1) / BBM) * ((N + BBN - 1) / BBN);
   auto a16 = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
-  return dtype == VTD_BF16 && e->out_dtype == VTD_BF16 && tiles >= kMinBigTiles && N > 64 &&
-         M % BBM == 0 && N % BBN == 0 && e->bias &&
-         e->scatter_tokens <= 0 && e->ldo % 8 == 0 && a16(e->out) && a16(e->bias) &&
-         (!e->resid || (e->ldr % 8 == 0 && a16(e->resid))) &&
-         (!e->out2 || (e->ldo2 % 8 == 0 && a16(e->out2))) && e->stat_ld >= N / 64 &&
-         reinterpret_cast<uintptr_t>(e->statout) % 8 == 0;
+  if (!(dtype == VTD_BF16 && e->out_dtype == VTD_BF16 && tiles >= kMinBigTiles && N > 64 &&
+        M % BBM == 0 && N % BBN == 0 && e->bias && e->statout &&
+        e->scatter_tokens <= 0 && e->ldo % 8 == 0 && a16(e->out) && a16(e->bias) &&
+        (!e->resid || (e->ldr % 8 == 0 && a16(e->resid))) &&
+        (!e->out2 || (e->ldo2 % 8 == 0 && a16(e->out2))) && e->stat_ld >= N / 64 &&
+        reinterpret_cast<uintptr_t>(e->statout) % 8 == 0))
+    return false;
+  return (pp2_code(e) & EPI_STAT) != 0 && pp2_code(e) != EPI_GENERIC;
 }
 
 // Whether vtd_gemm_mx8 can write its output as MX-fp8 (out_dtype VTD_FP8): the fast
@@ -1014,14 +1044,7 @@ void pp2_set_attributes() {
   once_per_device(once, [] {
 #define VTD_PP_FN(C) reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, false>), \
                      reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, true>),
-    const void* fns[] = {VTD_PP_FN(EPI_GENERIC) VTD_PP_FN(0) VTD_PP_FN(1) VTD_PP_FN(2)
-                         VTD_PP_FN(4) VTD_PP_FN(5) VTD_PP_FN(6) VTD_PP_FN(8) VTD_PP_FN(9)
-                         VTD_PP_FN(10) VTD_PP_FN(12) VTD_PP_FN(13) VTD_PP_FN(14)
-                         VTD_PP_FN(EPI_PARTIAL) VTD_PP_FN(4 | EPI_LNF) VTD_PP_FN(5 | EPI_LNF)
-                         VTD_PP_FN(6 | EPI_LNF) VTD_PP_FN(4 | EPI_STAT) VTD_PP_FN(5 | EPI_STAT)
-                         VTD_PP_FN(6 | EPI_STAT) VTD_PP_FN(12 | EPI_STAT)
-                         VTD_PP_FN(13 | EPI_STAT) VTD_PP_FN(14 | EPI_STAT)
-                         VTD_PP_FN(4 | EPI_STAT | EPI_RA) VTD_PP_FN(4 | EPI_RA)};
+    const void* fns[] = {VTD_PP_FN(EPI_GENERIC) VTD_PP2_CODES(VTD_PP_FN)};
 #undef VTD_PP_FN
     for (const void* f : fns)
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
@@ -1048,14 +1071,6 @@ __global__ __launch_bounds__(256) void gemm_splitk_epilogue_kernel(
 int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
                    int dtype, const vtd_epilogue* epi, hipStream_t stream, double flops,
                    const float* lnpart, int lnslots, int lnD, float lneps);
-
-// whether the pp2 kernel can take its fast (specialised) epilogues for this epilogue
-bool pp2_fast_epilogue(const vtd_epilogue* e) {
-  auto al16 = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
-  return e->bias && !e->detections && e->scatter_tokens <= 0 && e->ldo % 8 == 0 &&
-         (!e->resid || e->ldr % 8 == 0) && al16(e->out) && al16(e->bias) &&
-         (!e->resid || al16(e->resid)) && (!e->out2 || (e->ldo2 % 8 == 0 && al16(e->out2)));
-}
 
 int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
                 int dtype, const vtd_epilogue* epi, hipStream_t stream, double flops) {
@@ -1100,22 +1115,18 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
     const bf16_t* a16 = static_cast<const bf16_t*>(A);
     const bf16_t* b16 = static_cast<const bf16_t*>(Bt);
     const int ngw = tile_group_width(tiles_n);
+#if VTD_DIAG
     if (gemm_variant() == 12) {
       if (!gemm_w4_launch(M, N, K, a16, lda, b16, ldb, epi, ngw, stream))
         return fail(VTD_ERR_HIP, "gemm: w4 kernel attributes could not be set");
       VTD_LAUNCH_CHECK("gemm");
       return VTD_OK;
     }
+#endif
     pp2_set_attributes();
     EpiArgs e = make_epi_args(epi);
     e.ngw = ngw;
-    const bool fast = pp2_fast_epilogue(epi);
-    // the fold / statistics bits select their specialised epilogues; a combination without
-    // one (e.g. a fold with a residual) takes the generic epilogue, which reads both at run time
-    const int code = fast ? epi_code(e.act, e.out_dtype == VTD_BF16, e.resid != nullptr) |
-                                (e.lnstat ? EPI_LNF : 0) | (e.statout ? EPI_STAT : 0) |
-                                (e.rowadd ? EPI_RA : 0) | (e.out2 ? EPI_O2 : 0)
-                          : EPI_GENERIC;
+    const int code = pp2_code(epi);
     // transposed accumulators + register-direct epilogue for activation layers (mlp1 -5 %,
     // mlp2 -1.5 %), LDS-staged row vectors for the others (attn_out -10 %, mlp3 -4 %)
     const bool tr = e.act != VTD_ACT_NONE;
@@ -1123,12 +1134,7 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
     switch (code) {
 #define VTD_PP_CASE(C) \
   case C: pp2_launch<C>(tr, g, stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e); break;
-      VTD_PP_CASE(0) VTD_PP_CASE(1) VTD_PP_CASE(2) VTD_PP_CASE(4) VTD_PP_CASE(5) VTD_PP_CASE(6)
-      VTD_PP_CASE(8) VTD_PP_CASE(9) VTD_PP_CASE(10) VTD_PP_CASE(12) VTD_PP_CASE(13) VTD_PP_CASE(14)
-      VTD_PP_CASE(4 | EPI_LNF) VTD_PP_CASE(5 | EPI_LNF) VTD_PP_CASE(6 | EPI_LNF)
-      VTD_PP_CASE(4 | EPI_STAT) VTD_PP_CASE(5 | EPI_STAT) VTD_PP_CASE(6 | EPI_STAT)
-      VTD_PP_CASE(12 | EPI_STAT) VTD_PP_CASE(13 | EPI_STAT) VTD_PP_CASE(14 | EPI_STAT)
-      VTD_PP_CASE(4 | EPI_STAT | EPI_RA) VTD_PP_CASE(4 | EPI_RA)
+      VTD_PP2_CODES(VTD_PP_CASE)
 #undef VTD_PP_CASE
       default:
         pp2_launch<EPI_GENERIC>(tr, g, stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);
@@ -1154,11 +1160,10 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
 // round of the chip (kSplitTarget workgroups), every split keeping >= kSplitMinSteps K-steps
 // so its operand traffic stays well above its 256 KiB fp32 partial tile; 1 = no split.
 // Fixed targets (not the device's CU count) so that workspace sizing needs no device.
-// VTD_SPLITK=0 disables it (A/B switch, read per call).
+// VTD_SPLITK=0 / knob VTD_KNOB_SPLITK = 0 disables it.
 constexpr int kSplitTarget = 256, kSplitMinSteps = 8;
 int gemm_splitk_choice(int M, int N, int K, int dtype) {
-  const char* v = getenv("VTD_SPLITK");
-  if (v && atoi(v) == 0) return 1;
+  if (knob(VTD_KNOB_SPLITK) == 0) return 1;
   if (dtype != VTD_BF16 || N <= 64 || K % 64 != 0 || M <= 0) return 1;
   const int tiles = ((M + BBM - 1) / BBM) * ((N + BBN - 1) / BBN);
   const int nk = K / 64;
@@ -1178,6 +1183,9 @@ int gemm_splitk_launch(int M, int N, int K, const void* A, int lda, const void* 
   VTD_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 64 == 0 && N % 4 == 0,
                 "gemm_splitk: M, N, K positive, K % 64, N % 4");
   VTD_CHECK_ARG(A && Bt && epi && epi->out && part, "gemm_splitk: null pointer");
+  // the reduce kernel reads the partials as 16-B vectors (N % 4 keeps every row aligned)
+  VTD_CHECK_ARG(reinterpret_cast<uintptr_t>(part) % 16 == 0,
+                "gemm_splitk: part_dev must be 16-byte aligned");
   VTD_CHECK_ARG(lda >= K && ldb >= K && lda % 8 == 0 && ldb % 8 == 0,
                 "gemm_splitk: lda/ldb must be >= K and multiples of 8");
   VTD_CHECK_ARG(ksplit >= 2 && ksplit <= K / 64, "gemm_splitk: ksplit");
@@ -1195,7 +1203,7 @@ int gemm_splitk_launch(int M, int N, int K, const void* A, int lda, const void* 
   const bf16_t* a16 = static_cast<const bf16_t*>(A);
   const bf16_t* b16 = static_cast<const bf16_t*>(Bt);
   const dim3 g(tiles_m * tiles_n * ksplit);
-  if (N % 8 == 0 && reinterpret_cast<uintptr_t>(part) % 16 == 0)
+  if (N % 8 == 0)
     pp2_launch<EPI_PARTIAL>(false, g, stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, pe,
                             ksplit);
   else
@@ -1239,6 +1247,7 @@ int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_
   ProfScope ps(stream, PROF_GEMM, flops > 0 ? flops : 2.0 * M * N * (double)K);
   const int tiles_m = (M + BBM - 1) / BBM, tiles_n = (N + BBN - 1) / BBN;
   e.ngw = tile_group_width(tiles_n);
+#if VTD_DIAG
   // 3: x4 for the long-K layers (K >= 2048: the MLP's inner and last), ping-pong otherwise
   const int mxv = mx_variant();
   if (mxv == 2 || (mxv == 3 && K >= 2048)) {
@@ -1246,6 +1255,7 @@ int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_
     VTD_LAUNCH_CHECK("gemm_mx8");
     return VTD_OK;
   }
+#endif
   static std::once_flag once[kMaxDevices];
   once_per_device(once, [] {
 #define VTD_MX_FN(C) reinterpret_cast<const void*>(&gemm_mx8_pp_kernel<C>),
@@ -1313,3 +1323,8 @@ extern "C" int vtd_gemm_splitk(int M, int N, int K, const void* A_dev, int lda,
 extern "C" int vtd_gemm_splitk_choice(int M, int N, int K, int dtype) {
   return vtd::gemm_splitk_choice(M, N, K, dtype);
 }
+
+#if VTD_DIAG
+// present in the diagnostic build only (tests select the w4 / x4 comparisons by it)
+extern "C" int vtd_diag_build(void) { return 1; }
+#endif

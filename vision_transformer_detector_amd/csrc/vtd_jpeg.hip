@@ -1171,10 +1171,11 @@ int segments_of(const JpegDesc& d) {
   return d.restart ? (total + d.restart - 1) / d.restart : 1;
 }
 
-// Smallest chunk (bits); VTD_JPEG_CHUNK_BITS lowers it to stress the synchronisation.
+// Smallest chunk (bits); VTD_JPEG_CHUNK_BITS / knob VTD_KNOB_JPEG_CHUNK_BITS lowers it to
+// stress the synchronisation.
 int min_chunk_bits() {
-  const char* e = getenv("VTD_JPEG_CHUNK_BITS");
-  const int x = e ? atoi(e) : 1024;
+  const int k = knob(VTD_KNOB_JPEG_CHUNK_BITS);
+  const int x = k > 0 ? k : 1024;
   return std::max(64, x) / 32 * 32;
 }
 

@@ -54,6 +54,27 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+// ------------------------------------------------------------------ knobs
+namespace {
+constexpr const char* kKnobEnv[VTD_KNOB_COUNT] = {"VTD_ATTN_VARIANT", "VTD_ATTN_GRID",
+                                                  "VTD_GEMM_NGW", "VTD_SPLITK",
+                                                  "VTD_JPEG_CHUNK_BITS"};
+std::atomic<int> g_knob[VTD_KNOB_COUNT];
+std::once_flag g_knob_once;
+void knob_init() {
+  std::call_once(g_knob_once, [] {
+    for (int k = 0; k < VTD_KNOB_COUNT; ++k) {
+      const char* v = getenv(kKnobEnv[k]);
+      g_knob[k].store(v && *v ? atoi(v) : -1, std::memory_order_relaxed);
+    }
+  });
+}
+}  // namespace
+int knob(int k) {
+  knob_init();
+  return g_knob[k].load(std::memory_order_relaxed);
+}
+
 // ------------------------------------------------------------------ devices
 int current_device() {
   int dev = 0;
@@ -292,8 +313,16 @@ size_t split_workspace(const vtd_config* c, const vtd_dims& d) {
   }
   return std::max(total, whole);
 }
+// The side streams and the fork / join events are shared by every caller on a device, so
+// a split forward holds `mu` from its fork record to its join wait (calls are
+// re-entrant across host threads on distinct streams).  hipStreamWaitEvent orders the
+// waiting stream behind the event's latest record at the time of the wait call: another
+// thread's record in between would order this call's halves behind THAT caller's stream
+// position instead; and a side stream joined to a graph capture must carry nothing else
+// until its join.  The lock covers host-side enqueueing only (~1 ms per forward at C2).
 struct SideStream {
   int device = -1;
+  std::mutex mu;
   hipStream_t s[kMaxSplit - 1] = {};
   hipEvent_t fork = nullptr, join[kMaxSplit - 1] = {};
 };
@@ -334,6 +363,16 @@ using namespace vtd;
 extern "C" {
 
 int vtd_abi_version(void) { return VTD_ABI_VERSION; }
+
+int vtd_set_knob(int k, int value) {
+  VTD_CHECK_ARG(k >= 0 && k < VTD_KNOB_COUNT, "vtd_set_knob: unknown knob");
+  knob_init();
+  return g_knob[k].exchange(value, std::memory_order_relaxed);
+}
+int vtd_get_knob(int k) {
+  VTD_CHECK_ARG(k >= 0 && k < VTD_KNOB_COUNT, "vtd_get_knob: unknown knob");
+  return knob(k);
+}
 const char* vtd_last_error(void) { return g_last_error.c_str(); }
 
 int vtd_derive_dims(const vtd_config* cfg, vtd_dims* out) { return derive(cfg, out); }
@@ -370,7 +409,13 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
     // no side stream (first call under capture): the halves run in order on `st`
   }
   const size_t img = (size_t)cfg->image_h * cfg->image_w * cfg->channels;
-  if (side) VTD_HIP(hipEventRecord(side->fork, st));
+  // one caller at a time per device from the fork record to the join wait (SideStream)
+  std::unique_lock<std::mutex> side_lock;
+  if (side) side_lock = std::unique_lock<std::mutex>(side->mu);
+  if (side) {                       // fork: one record, every side stream waits on it
+    VTD_HIP(hipEventRecord(side->fork, st));
+    for (int part = 1; part < ns; ++part) VTD_HIP(hipStreamWaitEvent(side->s[part - 1], side->fork, 0));
+  }
   struct Part {
     vtd_config cfg;
     const float* images;
@@ -388,11 +433,7 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
     vtd_dims dp;
     rc = derive(&P.cfg, &dp);
     if (rc) return rc;
-    P.st = st;
-    if (side && part > 0) {
-      P.st = side->s[part - 1];
-      VTD_HIP(hipStreamWaitEvent(P.st, side->fork, 0));
-    }
+    P.st = side && part > 0 ? side->s[part - 1] : st;
     const size_t out_off = (size_t)b0 * VTD_MAX_DETECT * 6;
     P.images = images + b0 * img;
     P.logits = logits + out_off;
@@ -411,11 +452,12 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
       rc = forward_impl(&P.cfg, w, P.images, P.logits, P.dets, P.ws, P.st, s, s + 1, P.partials);
       if (rc) return rc;
     }
-  if (side)
+  if (side) {                       // join: each side stream's record and the caller's wait
     for (int part = 1; part < ns; ++part) {
       VTD_HIP(hipEventRecord(side->join[part - 1], side->s[part - 1]));
       VTD_HIP(hipStreamWaitEvent(st, side->join[part - 1], 0));
     }
+  }
   return VTD_OK;
 }
 }  // extern "C"
