@@ -114,14 +114,21 @@ def cpu_baseline(model, kw, shape, preset):
     the host cores: the reference's TF-CPU path cannot run in this pipeline (TF/Keras/tfa
     absent), so this is the "port" baseline.  SURVEY.md §8(d)'s plan: C1 (the
     reference default) and C2 (ViT-B/16 @224), batch 1 and 8, median of 5 forwards after 1
-    warm-up, torch's host threads (OMP_NUM_THREADS).  `value` = the bench preset's batch-8 median when it is one of
+    warm-up, len(os.sched_getaffinity(0)) host threads (capped by OMP_NUM_THREADS).  `value` = the bench preset's batch-8 median when it is one of
     the two (else C2's)."""
     import statistics
     import numpy as np
     import vision_transformer_detector_amd as vtd
     from oracle import vtd_numpy as ref
     from oracle.vtd_torch_cpu import TorchCpuDetector
-    threads = torch.get_num_threads()      # OMP_NUM_THREADS: the host-core share of this job
+    # SURVEY §8(d): torch.set_num_threads(len(os.sched_getaffinity(0))), capped by
+    # OMP_NUM_THREADS where the job's host-core share is set (16 per GPU on the GPU box,
+    # whose affinity mask shows the whole machine)
+    affinity = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(affinity, omp) if omp > 0 else affinity
+    prev_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
     cases = {}
     t_all = time.perf_counter()
     for name in ("c1", "vit_b16_224"):
@@ -143,12 +150,14 @@ def cpu_baseline(model, kw, shape, preset):
             med = statistics.median(ts)
             cases[f"{name}_b{b}"] = {"images_per_s": round(b / med, 3),
                                      "median_s": round(med, 4)}
+    torch.set_num_threads(prev_threads)
     key = f"{preset if preset in ('c1', 'vit_b16_224') else 'vit_b16_224'}_b8"
     return {"value": cases[key]["images_per_s"], "unit": "images/s", "cores": threads,
             "kind": "port",
             "sample": f"median of 5 forwards after 1 warm-up, batch 1 and 8, C1 (608x608 "
                       f"default) and C2 (ViT-B/16 @224), fp32 torch-CPU restatement, "
-                      f"{threads} threads, {time.perf_counter() - t_all:.1f} s in all; "
+                      f"{threads} threads (affinity {affinity}, OMP_NUM_THREADS "
+                      f"{omp or 'unset'}), {time.perf_counter() - t_all:.1f} s in all; "
                       f"value = {key}",
             "cases": cases}
 

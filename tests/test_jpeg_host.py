@@ -103,6 +103,25 @@ def test_progressive_header_walk(L, mode, kw):
     assert rc == 0 and ws > 0
 
 
+def test_progressive_dqt_redefined_after_its_scan_is_refused(L):
+    """libjpeg-turbo latches a component's quantization table at its first scan; a DQT that
+    redefines a latched table with other values between scans is refused by name,
+    one that repeats the same values is accepted."""
+    f = _jpeg(40, 48, "RGB", progressive=True, quality=75)
+    i = f.index(b"\xff\xdb")
+    ln = int.from_bytes(f[i + 2:i + 4], "big")
+    first = f[i + 4:i + 4 + 65]                 # Pq/Tq byte + 64 8-bit entries of table 0
+    assert first[0] >> 4 == 0
+    second_sos = f.index(b"\xff\xda", f.index(b"\xff\xda") + 2)
+    same = f[:second_sos] + _segment(0xDB, first) + f[second_sos:]
+    other = f[:second_sos] + _segment(0xDB, bytes([first[0]]) + bytes([1] * 64)) + f[second_sos:]
+    assert ln >= 67
+    rc, dims = _info(L, same)
+    assert rc == 0 and dims[:2] == (40, 48)
+    rc, _ = _info(L, other)
+    assert rc != 0 and b"latched" in L.lib.vtd_last_error()
+
+
 def _with_sof_sampling(f, comp0):
     """A copy of baseline JPEG f with component 0's sampling byte of the SOF0 replaced."""
     i = f.index(b"\xff\xc0")

@@ -198,6 +198,10 @@ bool parse_jpeg(const uint8_t* b, size_t n, JpegDesc& d, size_t& seg, size_t& se
   if (n < 4 || b[0] != 0xFF || b[1] != 0xD8) { err = "jpeg: no SOI marker"; return false; }
   RawHuff huff[8];
   bool qdef[4] = {}, frame = false;
+  // libjpeg-turbo latches a component's quantization table at the component's first scan
+  // (jdinput.c latch_quant_tables); a progressive file redefining a latched table with other
+  // values afterwards would need per-component copies: refused
+  bool latched[4] = {};
   int nscans = 0;
   size_t pos = 2;
   auto u16 = [&](size_t at) { return (int)b[at] << 8 | b[at + 1]; };
@@ -228,6 +232,10 @@ bool parse_jpeg(const uint8_t* b, size_t n, JpegDesc& d, size_t& seg, size_t& se
         if (tq > 3 || pq > 1 || p + 64 * (pq + 1) > e) { err = "jpeg: bad DQT"; return false; }
         for (int k = 0; k < 64; ++k) {
           const int v = pq ? u16(p + 2 * k) : b[p + k];
+          if (latched[tq] && d.q[tq][kZigzagToNatural[k]] != (uint16_t)v) {
+            err = "jpeg: quantization table redefined after a scan latched it (not supported)";
+            return false;
+          }
           d.q[tq][kZigzagToNatural[k]] = (uint16_t)v;
         }
         p += 64 * (pq + 1);
@@ -364,6 +372,11 @@ bool parse_jpeg(const uint8_t* b, size_t n, JpegDesc& d, size_t& seg, size_t& se
       for (int i = 0; i < ntab; ++i) {
         const int t = dc ? td[i] : ta[0] + 4;
         if (!huff[t].present) { err = "jpeg: missing Huffman table"; return false; }
+      }
+      for (int i = 0; i < ns; ++i) {
+        const int tq = d.comp[idx[i]].tq;
+        if (!qdef[tq]) { err = "jpeg: missing quantization table"; return false; }
+        latched[tq] = true;
       }
       const size_t end = scan_end(b, e, n);
       if (scans) {

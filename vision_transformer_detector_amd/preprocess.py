@@ -68,9 +68,10 @@ def get_image_tensors(images, target_height: int = MODEL_IMAGE_HEIGHT,
 def decode_jpegs(files, device="cuda", stream=None):
     """JPEG file bytes (a list of `bytes`) -> (packed RGB uint8 pixels on `device`, per-image
     byte offsets (int64, host), [(height, width), ...]): `tf.image.decode_image(f, channels=3)`
-    (vision_transformer_utilities.py:431) for baseline JPEGs, decoded on the device by
-    vtd_jpeg_decode.  Unsupported JPEG flavours (progressive, CMYK, 12-bit) raise
-    ValueError naming the reason; nothing falls back to a host decoder."""
+    (vision_transformer_utilities.py:431) for baseline / extended sequential and progressive
+    Huffman JPEGs, decoded on the device by vtd_jpeg_decode.  Unsupported JPEG flavours
+    (arithmetic-coded, lossless, 12-bit, 4:4:0, CMYK / YCCK) raise ValueError naming the
+    reason; nothing falls back to a host decoder."""
     import ctypes
     if len(files) == 0:
         raise ValueError("decode_jpegs: empty file list")
