@@ -190,8 +190,13 @@ def _attn_ref(qkv, B, N, H, dk, dkp):
                                       # persistent kernel (dkp 64, 128 < N <= 256): several
                                       # pairs per workgroup, N not a multiple of 32 / 8
                                       (40, 196, 12, 64), (3, 129, 5, 64), (2, 256, 2, 64),
-                                      (1, 200, 3, 50), (700, 131, 1, 64), (2, 224, 3, 64)])
-def test_attention(L, cuda, dtype, B, N, H, dk):
+                                      (1, 200, 3, 50), (700, 131, 1, 64), (2, 224, 3, 64),
+                                      # 16-query persistent kernel (N in (192, 208])
+                                      (300, 193, 1, 64), (3, 208, 5, 64)])
+@pytest.mark.parametrize("variant", [-1, 5])
+def test_attention(L, cuda, dtype, B, N, H, dk, variant):
+    if variant != -1 and (dtype != "bf16" or dk > 64 or not 192 < N <= 256):
+        pytest.skip("the variant applies to bf16, dkp 64, N in (192, 256] only")
     code, tdt = _dt(L, dtype)
     dkp = 32 if dk <= 32 else (64 if dk <= 64 else 128)
     ld = 3 * H * dkp + 8
@@ -205,9 +210,10 @@ def test_attention(L, cuda, dtype, B, N, H, dk):
     ldo = H * dkp
     out = torch.full((B * N, ldo), float("nan"), dtype=tdt, device=cuda)
     qkv_d = qkv_t.to(cuda)
-    L.check(L.lib.vtd_attention(qkv_d.data_ptr(), B, N, H, dkp, ld,
-                                1.0 / math.sqrt(dk), out.data_ptr(), ldo, code,
-                                L.stream_ptr()), "attention")
+    with L.knob(L.KNOB_ATTN_VARIANT, variant):
+        L.check(L.lib.vtd_attention(qkv_d.data_ptr(), B, N, H, dkp, ld,
+                                    1.0 / math.sqrt(dk), out.data_ptr(), ldo, code,
+                                    L.stream_ptr()), "attention")
     torch.cuda.synchronize()
     exp = _attn_ref(qkv_t.double().numpy(), B, N, H, dk, dkp)
     got = out.cpu().double().numpy().reshape(B, N, H, dkp)
@@ -217,7 +223,8 @@ def test_attention(L, cuda, dtype, B, N, H, dk):
     assert (got[..., dk:] == 0).all()
 
 
-@pytest.mark.parametrize("B,N,H", [(256, 196, 12), (5, 129, 7), (3, 224, 4), (1, 161, 1)])
+@pytest.mark.parametrize("B,N,H", [(256, 196, 12), (5, 129, 7), (3, 224, 4), (1, 161, 1),
+                                   (7, 193, 3), (2, 208, 2)])
 def test_attention_persistent_equals_per_pair_kernel(L, cuda, monkeypatch, B, N, H):
     """The persistent short-sequence kernel (knob VTD_KNOB_ATTN_VARIANT 4, the default for dkp 64 and
     128 < N <= 256) against the per-(image, head) kernel, at the C2 shape (3072 pairs, 12 per
@@ -230,17 +237,19 @@ def test_attention_persistent_equals_per_pair_kernel(L, cuda, monkeypatch, B, N,
     g = torch.Generator().manual_seed(N + H)
     qkv = (torch.randn(B * N, ld, generator=g) * 1.5).to(torch.bfloat16).to(cuda)
     outs = []
-    for variant in (2, 4):
+    for variant in (2, 4, 5):
         o = torch.full((B * N, H * dkp + 16), float("nan"), dtype=torch.bfloat16, device=cuda)
         with L.knob(L.KNOB_ATTN_VARIANT, variant):
             L.check(L.lib.vtd_attention(qkv.data_ptr(), B, N, H, dkp, ld, 0.125, o.data_ptr(),
                                         H * dkp + 16, L.BF16, L.stream_ptr()), "attention")
         torch.cuda.synchronize()
         outs.append(o.cpu())
-    a, b = outs[0][:, :H * dkp].float(), outs[1][:, :H * dkp].float()
-    assert torch.isfinite(b).all()
-    assert (a - b).abs().max().item() <= 1e-2 * max(1.0, a.abs().max().item())
-    assert torch.isnan(outs[1][:, H * dkp:].float()).all()     # nothing written past ldo's heads
+    a = outs[0][:, :H * dkp].float()
+    for o in outs[1:]:
+        b = o[:, :H * dkp].float()
+        assert torch.isfinite(b).all()
+        assert (a - b).abs().max().item() <= 1e-2 * max(1.0, a.abs().max().item())
+        assert torch.isnan(o[:, H * dkp:].float()).all()     # nothing written past ldo's heads
 
 
 def test_attention_uniform_kat(L, cuda):

@@ -2,8 +2,9 @@
   - vtd_quantize_mx8 against the CPU restatement oracle/mx8.py, element for element
     (e4m3 values and E8M0 block exponents must be identical);
   - vtd_gemm_mx8 against the fp64 product of the DEQUANTIZED device operands, so the
-    check isolates the block-scaled MFMA + fp32 accumulation + epilogue; both MX kernels
-    (VTD_MX_VARIANT 1 = 8-wave ping-pong, 2 = x4, one wave per SIMD).  Tolerance
+    check isolates the block-scaled MFMA + fp32 accumulation + epilogue; the 8-wave
+    ping-pong kernel (and, with the diagnostic library, VTD_MX_VARIANT 2 = x4, one wave per
+    SIMD).  Tolerance
     5e-4 relative for f32 outputs: the instruction reduces each 128-element K-step
     inside the matrix core before the fp32 accumulate (measured max 1.1e-4 at K <= 1536,
     6x the 2e-5 of the bf16 MFMA's exact fp32 fma chain); 8e-3 for bf16 outputs.
@@ -22,15 +23,15 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
+def L(cuda):
+    from vision_transformer_detector_amd import _lib
+    return _lib
+
 
 def _need_variant(L, variant):
     """VTD_MX_VARIANT 2 / 3 (the x4 kernel) exist in the diagnostic library only."""
     if variant != "1" and not hasattr(L.lib, "vtd_diag_build"):
         pytest.skip("the x4 kernel is in the diagnostic build only (make diag)")
-
-def L(cuda):
-    from vision_transformer_detector_amd import _lib
-    return _lib
 
 
 def _quantize(L, x, Kq, s_rows=None):

@@ -1,6 +1,7 @@
 """Attention kernel micro-benchmark through the C-ABI at the C2 shape (B=256, N=196, 12
-heads x 64, bf16), for rocprofv3 PMC passes and variant A/B (VTD_ATTN_VARIANT).
-  python tools/attn_bench.py [--reps 20] [--B 256] [--N 196] [--flush]"""
+heads x 64, bf16), for rocprofv3 PMC passes and variant A/B (knob VTD_KNOB_ATTN_VARIANT,
+interleaved rounds in one process).
+  python tools/attn_bench.py [--reps 20] [--B 256] [--N 196] [--flush] [--variants 4,5] [--rounds 3]"""
 import argparse
 import json
 import math
@@ -20,6 +21,8 @@ def main():
     ap.add_argument("--N", type=int, default=196)
     ap.add_argument("--H", type=int, default=12)
     ap.add_argument("--flush", action="store_true", help="evict the MALL between reps")
+    ap.add_argument("--variants", default="-1")
+    ap.add_argument("--rounds", type=int, default=1)
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     B, N, H, dkp = a.B, a.N, a.H, 64
@@ -31,25 +34,27 @@ def main():
     st = L.stream_ptr()
     call = lambda: L.check(L.lib.vtd_attention(qkv.data_ptr(), B, N, H, dkp, ld, 1 / math.sqrt(64),
                                                out.data_ptr(), H * dkp, L.BF16, st))
-    for _ in range(3):
-        call()
     t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ms = 0.0
-    for _ in range(a.reps):
-        if junk is not None:
-            junk.fill_(1)
-        t0.record()
-        call()
-        t1.record()
-        torch.cuda.synchronize()
-        ms += t0.elapsed_time(t1)
-    us = 1e3 * ms / a.reps
-    byts = B * N * (ld + H * dkp) * 2
-    print(json.dumps({"variant": os.environ.get("VTD_ATTN_VARIANT", "default"), "B": B, "N": N,
-                      "flush": a.flush, "us": round(us, 2),
-                      "hbm_tbs": round(byts / us / 1e6, 2),
-                      "tflops": round(4.0 * B * H * N * N * 64 / us / 1e6, 1)}), flush=True)
-
+    for rnd in range(a.rounds):
+        for v in [int(x) for x in a.variants.split(",")]:
+            with L.knob(L.KNOB_ATTN_VARIANT, v):
+                for _ in range(3):
+                    call()
+                ms = 0.0
+                for _ in range(a.reps):
+                    if junk is not None:
+                        junk.fill_(1)
+                    t0.record()
+                    call()
+                    t1.record()
+                    torch.cuda.synchronize()
+                    ms += t0.elapsed_time(t1)
+            us = 1e3 * ms / a.reps
+            byts = B * N * (ld + H * dkp) * 2
+            print(json.dumps({"variant": v, "round": rnd, "B": B, "N": N,
+                              "flush": a.flush, "us": round(us, 2),
+                              "hbm_tbs": round(byts / us / 1e6, 2),
+                              "tflops": round(4.0 * B * H * N * N * 64 / us / 1e6, 1)}), flush=True)
 
 if __name__ == "__main__":
     main()

@@ -26,7 +26,21 @@ SHAPES = {  # name: (M, N, K, act, out_dtype, resid)
     # diagnostics: the activation's share of an epilogue (mlp1 / mlp2 without GELU)
     "mlp1_noact": (50176, 3072, 768, 0, 1, False),
     "mlp2_noact": (50176, 1536, 3072, 0, 1, False),
+    # the forward's own epilogues: residual layers emitting the next LayerNorm's partial
+    # statistics (statout), LayerNorm-folded consumers (lnstat / colsum)
+    "attn_out_st": (50176, 768, 768, 0, 1, True),
+    "mlp3_st": (50176, 768, 1536, 1, 1, True),
+    "qkv_ln": (50176, 2304, 768, 0, 1, False),
+    "mlp1_ln": (50176, 3072, 768, 1, 1, False),
+    # the micro-batch halves of the two-stream forward (B = 128 each)
+    "attn_out_h": (25088, 768, 768, 0, 1, True),
+    "mlp3_h": (25088, 768, 1536, 1, 1, True),
+    "qkv_h": (25088, 2304, 768, 0, 1, False),
+    "mlp1_h": (25088, 3072, 768, 1, 1, False),
+    "mlp2_h": (25088, 1536, 3072, 1, 1, False),
 }
+STATOUT = {"attn_out_st", "mlp3_st"}
+LNFOLD = {"qkv_ln", "mlp1_ln"}
 
 
 def run(name, spec, reps, dev):
@@ -42,6 +56,16 @@ def run(name, spec, reps, dev):
     e.out, e.ldo, e.out_dtype = out.data_ptr(), N, od
     if res:
         e.resid, e.ldr = out.data_ptr(), N
+    keep = []
+    if name in STATOUT:
+        stat = torch.empty(M, N // 64, 2, device=dev)
+        keep.append(stat)
+        e.statout, e.stat_ld = stat.data_ptr(), N // 64
+    if name in LNFOLD:
+        lnstat = torch.stack([torch.zeros(M, device=dev), torch.ones(M, device=dev)], 1).contiguous()
+        colsum = Bt.float().sum(1).contiguous()
+        keep += [lnstat, colsum]
+        e.lnstat, e.colsum = lnstat.data_ptr(), colsum.data_ptr()
     st = L.stream_ptr()
     call = lambda: L.check(L.lib.vtd_gemm(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K,
                                           L.BF16, ctypes.byref(e), st))

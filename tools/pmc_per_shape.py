@@ -26,7 +26,8 @@ def shape_of(kernel, grid):
     wg = grid // 512 if grid % 512 == 0 else grid
     resid = "<76" in kernel or "<77" in kernel or "<12" in kernel or "<13" in kernel or "<14" in kernel
     for name, (M, N, K, act, od, res) in SHAPES.items():
-        if tiles(M, N) == wg and res == resid and not name.endswith("_noact"):
+        if (tiles(M, N) == wg and res == resid and not name.endswith("_noact") and
+                not name.endswith(("_st", "_ln"))):
             return name
     return f"{kernel[:40]}|{wg}"
 

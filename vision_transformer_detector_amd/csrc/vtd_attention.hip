@@ -18,6 +18,7 @@
 #include <stdlib.h>
 
 #include <type_traits>
+#include <utility>
 
 #include "vtd_common.h"
 
@@ -735,6 +736,256 @@ __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ---------------------------------------------------------------------------------
+// Persistent short-sequence kernel, 16 queries per wave (bf16, DKP = 64, N in
+// (16 (NKB - 1), 16 NKB]; the C2 shape N = 196 is NKB = 13).  The 32-query kernel above runs
+// 2 waves per SIMD (7 active of 8 at N = 196) with ~190 registers each: its softmax chains
+// (a 56-deep max, exponentials feeding the PV MFMAs) have little else to hide behind.  Here a
+// workgroup has NKB waves (one 16-query block each, every wave active at N = 196) with
+// <= 128 registers: 3-4 waves per SIMD.  v_mfma_f32_16x16x32_bf16 throughout:
+//   S^T block kb (16 keys x 16 queries) = K[16 kb .. +15] . Q^T: lane l holds query
+//   q0 + (l & 15) and keys 16 kb + 4 g + r (g = l >> 4, r = 0..3);
+//   O^T (64 d x 16 queries) += V^T . P^T per 32-key step ks: P^T's 8 K-elements of lane l are
+//   its own scores of blocks 2 ks and 2 ks + 1 (keys 16 (2ks) + 4g + 0..3 and
+//   16 (2ks + 1) + 4g + 0..3, all lane-local), and V^T's are the same keys at d = 16 db +
+//   (l & 15), two ds_read_b64_tr_b16 (one 4-key x 16-d block per 16-lane group);
+//   row max / sum: in-lane trees, then the four lanes l, l ^ 16, l ^ 32, l ^ 48 of a query
+//   (gfx950 lane swaps).
+// Loads as in the 32-query kernel: K / V of a pair (N rounded up to 32 rows of 128 B: an odd
+// last 16-key block pairs with zero P against clamped, finite V rows) by LDS-DMA into one of
+// two slots one pair ahead, Q one pair ahead; O restaged through the pair's slot and stored
+// as whole 128-B rows (buffer range check drops rows >= N): 2 stores per wave, `vmcnt(2)`.
+// LDS images (swizzle on the DMA source): K, Q rows chunk ^ ((row >> 1) & 7) (the 16 rows x
+// 16 B of every ds_read_b128 lane group hit 16 distinct bank slots for this read pattern);
+// V rows chunk ^ (((row >> 1) & 3) << 1) (the 8 rows x 32 B of a tr-read half-wave cover the
+// 64 banks once).  Same operations per score / output as attention_bf16_ps_kernel, summed in
+// another order: equal to within fp32 / bf16-P rounding (tested against it and fp64).
+__device__ __forceinline__ int swz_v16(int row) { return ((row >> 1) & 3) << 1; }
+__device__ __forceinline__ float xmax16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xadd16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false,
+                                                  false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// f(integral_constant<int, I>) for I in the sequence, in order (compile-time indices)
+template <int... I, class F>
+__device__ __forceinline__ void static_for(std::integer_sequence<int, I...>, F&& f) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+
+template <int OFF>
+__device__ __forceinline__ bf16x4 tr_read(uint32_t a) {
+  bf16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(a), "n"(OFF));
+  return v;
+}
+
+template <int NKB>
+__global__ __launch_bounds__(1024, 1) void attention_bf16_ps16_kernel(
+    const bf16_t* __restrict__ qkv, int npairs, int N, int heads, int ldqkv, float scale_log2,
+    bf16_t* __restrict__ out, int ldo) {
+  constexpr int DKP = 64;
+  constexpr int NKS = (NKB + 1) / 2;             // 32-key PV steps
+  constexpr int NR = 32 * NKS;                   // LDS rows per matrix
+  constexpr int SLOT = 2 * NR * 128;             // K image, then V image
+  constexpr int NG = NR / 8;                     // 8-row DMA groups per matrix
+  typedef __attribute__((address_space(3))) void lds_void_t;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6, fr = lane & 15, g = lane >> 4;
+  char* const qarea = smem + 2 * SLOT;
+  const int inner = heads * DKP;
+  const int q0 = wave * 16;
+  const int G = gridDim.x;
+  const int lrow = lane >> 3, lchunk = lane & 7;
+  const uint32_t lds_base =
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(smem);
+
+  // DMA of one matrix (part 0 = Q, 1 = K, 2 = V) of pair p into dst
+  auto issue = [&](int p, int part, char* dst) {
+    const int b = p / heads, h = p - b * heads;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(qkv + (int64_t)b * N * ldqkv), 0, N * ldqkv * 2, 0x00020000);
+    const int colb = (part * inner + h * DKP) * 2;
+    for (int gi = wave; gi < NG; gi += NKB) {
+      const int r = gi * 8 + lrow;
+      const int sw = part == 2 ? swz_v16(r) : swz_kq(r);
+      const int voff = min(r, N - 1) * ldqkv * 2 + colb + ((lchunk ^ sw) << 4);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + gi * 1024), 16, voff, 0,
+                                               0, 0);
+    }
+  };
+
+  int p = blockIdx.x;
+  if (p >= npairs) return;                       // uniform per workgroup
+  issue(p, 1, smem);
+  issue(p, 2, smem + NR * 128);
+  issue(p, 0, qarea);
+  // lane-constant pieces of the LDS addresses
+  const int skq = (fr >> 1) & 7;                 // swz_kq of rows 16 kb + fr and q0 + fr
+  const int tr_row = 4 * g + (fr >> 2);          // tr-read: key row within a 16-key block
+  const int tr_p = fr & 3;                       // tr-read: 4-d piece within the 16-d block
+  const int swv = swz_v16(tr_row);               // (row >> 1) & 3: independent of the block
+  for (int it = 0; p < npairs; p += G, ++it) {
+    char* const kl = smem + (it & 1) * SLOT;
+    const uint32_t kl_addr = lds_base + (it & 1) * SLOT, vl_addr = kl_addr + NR * 128;
+    if (it == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");   // previous pair's O stores may fly
+    __builtin_amdgcn_s_barrier();
+    bf16x8 qf[2];
+    {
+      const int row = q0 + fr;
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+        qf[st] = *reinterpret_cast<const bf16x8*>(qarea + row * 128 + (((4 * st + g) ^ skq) << 4));
+    }
+    const int pn = p + G;
+    const bool fetch = pn < npairs;
+    if (fetch) {
+      char* const kn = smem + ((it + 1) & 1) * SLOT;
+      issue(pn, 1, kn);
+      issue(pn, 2, kn + NR * 128);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // Q fragments in registers
+    __builtin_amdgcn_s_barrier();
+    if (fetch) issue(pn, 0, qarea);
+
+    // ---- S^T blocks: all NKB at once (independent 2-MFMA chains); the row max as a tree
+    f32x4 s[2 * NKS];
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+      s[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const char* krow = kl + (kb * 16 + fr) * 128;
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+        s[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            *reinterpret_cast<const bf16x8*>(krow + (((4 * st + g) ^ skq) << 4)), qf[st], s[kb],
+            0, 0, 0);
+    }
+    if (N < NKB * 16) {                          // keys >= N of the last block
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if ((NKB - 1) * 16 + 4 * g + r >= N) s[NKB - 1][r] = -INFINITY;
+    }
+    float bm[NKB];
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb)
+      bm[kb] = fmaxf(fmaxf(s[kb][0], s[kb][1]), fmaxf(s[kb][2], s[kb][3]));
+#pragma unroll
+    for (int w = 1; w < NKB; w *= 2)
+#pragma unroll
+      for (int kb = 0; kb + w < NKB; kb += 2 * w) bm[kb] = fmaxf(bm[kb], bm[kb + w]);
+    const float mx = xmax16(pair_max(bm[0])) * scale_log2;
+    const float nmx = -mx;
+    // ---- P = exp2(S c - max), O^T += V^T . P^T per 32-key step; V^T by tr-reads (inline
+    // asm: the compiler's tr-read would wait for the in-flight DMA), offsets immediate
+    f32x4 o[4];
+#pragma unroll
+    for (int db = 0; db < 4; ++db) o[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint32_t va[4];
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+      va[db] = vl_addr + tr_row * 128 + (((2 * db + (tr_p >> 1)) ^ swv) << 4) + (tr_p & 1) * 8;
+    float ps[4] = {0.f, 0.f, 0.f, 0.f};
+    auto step = [&](auto ks_tag) {
+      constexpr int ks = decltype(ks_tag)::value;
+      bf16x4 lo[4], hi[4];
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        lo[db] = tr_read<ks * 4096>(va[db]);
+        hi[db] = tr_read<ks * 4096 + 2048>(va[db]);
+      }
+      float e[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        e[j] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[2 * ks][j], scale_log2, nmx));
+        ps[j] += e[j];
+      }
+      if constexpr (2 * ks + 1 < NKB) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          e[4 + j] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[2 * ks + 1][j], scale_log2, nmx));
+          ps[j] += e[4 + j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) e[4 + j] = 0.f;   // the odd block past the last: P = 0
+      }
+      const bf16x8 pb = __builtin_bit_cast(bf16x8, i32x4{(int)pack_bf16x2(e[0], e[1]),
+                                                         (int)pack_bf16x2(e[2], e[3]),
+                                                         (int)pack_bf16x2(e[4], e[5]),
+                                                         (int)pack_bf16x2(e[6], e[7])});
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const bf16x8 a = {lo[db][0], lo[db][1], lo[db][2], lo[db][3],
+                          hi[db][0], hi[db][1], hi[db][2], hi[db][3]};
+        o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb, o[db], 0, 0, 0);
+      }
+    };
+    static_for(std::make_integer_sequence<int, NKS>{}, step);
+    const float l_run = (ps[0] + ps[1]) + (ps[2] + ps[3]);
+    // every wave done reading this slot's K / V: restage O in it, store whole rows
+    __builtin_amdgcn_s_barrier();
+    const float inv = 1.f / xadd16(pair_sum(l_run));
+    char* const wst = kl + wave * (16 * 144);
+    {
+      // lane: query row fr, d = 16 db + 4 g + 0..3 -> 8 B at byte 32 db + 8 g
+      const uint32_t wa = kl_addr + wave * (16 * 144) + fr * 144 + 8 * g;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const uint2 v = {pack_bf16x2(o[db][0] * inv, o[db][1] * inv),
+                         pack_bf16x2(o[db][2] * inv, o[db][3] * inv)};
+        if (db == 0) asm volatile("ds_write_b64 %0, %1 offset:0" ::"v"(wa), "v"(v) : "memory");
+        if (db == 1) asm volatile("ds_write_b64 %0, %1 offset:32" ::"v"(wa), "v"(v) : "memory");
+        if (db == 2) asm volatile("ds_write_b64 %0, %1 offset:64" ::"v"(wa), "v"(v) : "memory");
+        if (db == 3) asm volatile("ds_write_b64 %0, %1 offset:96" ::"v"(wa), "v"(v) : "memory");
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // wave-local: own writes landed
+    {
+      const int b = p / heads, h = p - b * heads;
+      const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+          out + (int64_t)b * N * ldo, 0, N * ldo * 2, 0x00020000);
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+        const int r = pass * 8 + lrow;
+        const i32x4 v = *reinterpret_cast<const i32x4*>(wst + r * 144 + lchunk * 16);
+        // rows >= N fall outside the range: dropped
+        __builtin_amdgcn_raw_buffer_store_b128(v, ro, ((q0 + r) * ldo + h * DKP + lchunk * 8) * 2,
+                                               0, 0);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+int launch_bf16_ps16(const void* qkv, int B, int N, int heads, int ldqkv, float scale,
+                     void* out, int ldo, hipStream_t stream) {
+  constexpr int NKB = 13;                        // N in (192, 208]: C2 (N = 196)
+  constexpr int NR = 32 * ((NKB + 1) / 2);
+  constexpr int lds = 5 * NR * 128;
+  static std::once_flag once[kMaxDevices];
+  once_per_device(once, [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_bf16_ps16_kernel<NKB>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  });
+  const int npairs = B * heads;
+  const int kg = knob(VTD_KNOB_ATTN_GRID);
+  const int grid = std::min(npairs, kg > 0 ? kg : device_cu_count());
+  hipLaunchKernelGGL(attention_bf16_ps16_kernel<NKB>, dim3(grid), dim3(64 * NKB), lds, stream,
+                     static_cast<const bf16_t*>(qkv), npairs, N, heads, ldqkv,
+                     scale * 1.4426950408889634f, static_cast<bf16_t*>(out), ldo);
+  VTD_LAUNCH_CHECK("attention_bf16_ps16");
+  return VTD_OK;
+}
+
 int launch_bf16_ps(const void* qkv, int B, int N, int heads, int ldqkv, float scale, void* out,
                    int ldo, hipStream_t stream) {
   const int NR = (N + 31) & ~31;
@@ -830,8 +1081,12 @@ int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqk
     const int v1 = kv >= 0 ? kv : 4;
     // 4 (default): the persistent kernel where it applies (dkp 64, 128 < N <= 256, whole
     // 128-B rows and 16-B aligned row pitches), else as 2
-    if (v1 == 4 && dkp == 64 && N > 128 && N <= 256 && ldqkv % 8 == 0 && ldo % 8 == 0 &&
-        (int64_t)N * ldqkv * 2 < INT32_MAX && (int64_t)N * ldo * 2 < INT32_MAX)
+    const bool ps_ok = dkp == 64 && N > 128 && N <= 256 && ldqkv % 8 == 0 && ldo % 8 == 0 &&
+                       (int64_t)N * ldqkv * 2 < INT32_MAX && (int64_t)N * ldo * 2 < INT32_MAX;
+    // 5: the 16-query-per-wave persistent kernel at N in (192, 208] (C2), else as 4
+    if (v1 == 5 && ps_ok && N > 192 && N <= 208)
+      return launch_bf16_ps16(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+    if ((v1 == 4 || v1 == 5) && ps_ok)
       return launch_bf16_ps(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
     if (v1 == 1) {
       if (dkp == 32) return launch<bf16_t, 32>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);

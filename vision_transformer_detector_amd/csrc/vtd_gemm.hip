@@ -164,15 +164,17 @@ typedef __attribute__((address_space(1))) const void gbl_void_t;
 // Writes the wave's 128 x 64 accumulator tile: 4 passes of 32 rows staged through the
 // wave's private LDS region; each lane then owns 8 consecutive columns of a row, so
 // residual reads and output writes are 16-B per lane (one 128-B line per 8 lanes).
-template <int EPI, int PR = 32>
+// DG (diagnostic build only, wrong outputs): 1 = no partial statistics, 2 = no residual
+// loads, 4 = no output stores (values kept live), 8 = no epilogue at all
+template <int EPI, int PR = 32, int DG = 0>
 __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* ep, int lane,
                                               int m_base, int n_base, const EpiArgs& e,
                                               const float2* lst = nullptr) {
   constexpr int ACT = EPI & 3;
   constexpr bool OUT_BF16 = (EPI & 4) != 0;
-  constexpr bool RESID = (EPI & 8) != 0;
+  constexpr bool RESID = (EPI & 8) != 0 && !(DG & 2);
   constexpr bool NOBIAS = (EPI & EPI_PARTIAL) != 0;   // split-K partial: raw fp32 sums
-  constexpr bool LNF = (EPI & EPI_LNF) != 0, STAT = (EPI & EPI_STAT) != 0;
+  constexpr bool LNF = (EPI & EPI_LNF) != 0, STAT = (EPI & EPI_STAT) != 0 && !(DG & 1);
   constexpr bool F8O = (EPI & EPI_F8O) != 0;
   constexpr int ES = 68;
   constexpr int NB = PR / 16;            // accumulator row blocks per pass
@@ -272,7 +274,8 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
         }
         const i32x4 o = {(int)pack_bf16x2(v0[0], v0[1]), (int)pack_bf16x2(v0[2], v0[3]),
                          (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
-        store_out16(static_cast<bf16_t*>(e.out) + idx, o);
+        if constexpr (DG & 4) asm volatile("" ::"v"(o));
+        else store_out16(static_cast<bf16_t*>(e.out) + idx, o);
         if constexpr (STAT) {      // the row's 64 columns live in 8 consecutive lanes
           // block mean, then the centred sum of squares (DPP sums, no LDS traffic)
           const float mean = sum8_dpp(bf16x8_sum(o)) * (1.f / 64.f);
@@ -544,14 +547,14 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
 // for accumulator row block i and column half jp, output row m_base + 16 i + fr and the 8
 // contiguous columns n_base + 32 jp + 8 fg + 0..7 (acc[i][2 jp] = first 4, acc[i][2 jp + 1]
 // = last 4).  Bias is loaded once; residual rows are fetched 4 row blocks at a time.
-template <int EPI>
+template <int EPI, int DG = 0>
 __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int lane, int m_base,
                                                 int n_base, const EpiArgs& e,
                                                 const float2* lst = nullptr) {
   constexpr int ACT = EPI & 3;
   constexpr bool OUT_BF16 = (EPI & 4) != 0;
-  constexpr bool RESID = (EPI & 8) != 0;
-  constexpr bool LNF = (EPI & EPI_LNF) != 0, STAT = (EPI & EPI_STAT) != 0;
+  constexpr bool RESID = (EPI & 8) != 0 && !(DG & 2);
+  constexpr bool LNF = (EPI & EPI_LNF) != 0, STAT = (EPI & EPI_STAT) != 0 && !(DG & 1);
   const int fr = lane & 15, fg = lane >> 4;
   f32x4 bias[2][2], cs[2][2] = {};
 #pragma unroll
@@ -618,7 +621,8 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
         if constexpr (OUT_BF16) {
           const i32x4 o = {(int)pack_bf16x2(v0[0], v0[1]), (int)pack_bf16x2(v0[2], v0[3]),
                            (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
-          store_out16(static_cast<bf16_t*>(e.out) + idx, o);
+          if constexpr (DG & 4) asm volatile("" ::"v"(o));
+          else store_out16(static_cast<bf16_t*>(e.out) + idx, o);
           if constexpr (STAT) {
             ob[jp] = o;
             tsum += bf16x8_sum(o);
@@ -669,7 +673,7 @@ __device__ __forceinline__ void epilogue_direct_generic(const f32x4 (&acc)[8][4]
 // v % tiles (neighbours on an XCD share a K range, so their panels are the same lines) and
 // writes its fp32 partial tile at e.out + split * e.split_stride; gemm_splitk_epilogue_kernel
 // sums the splits and applies the layer's epilogue.
-template <int EPI, bool TR = false>
+template <int EPI, bool TR = false, int DG = 0>
 __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
     int M, int N, int K, const bf16_t* __restrict__ A, int lda,
     const bf16_t* __restrict__ Bt, int ldb, int tiles_m, int tiles_n, EpiArgs e, int ksplit) {
@@ -706,10 +710,17 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
   const int fr = lane & 15, fg = lane >> 4;
   pp2_mainloop<TR>(acc, smem, src, nk, wave, wm, wn, fr, fg);
   const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
+  if constexpr ((DG & 8) != 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
   if constexpr (TR) {
     if constexpr (EPI != EPI_GENERIC) {
       if (m0 + BBM <= M && n0 + BBN <= N) {
-        epilogue_direct<EPI>(acc, lane, m_base, n_base, e, lst);
+        epilogue_direct<EPI, DG>(acc, lane, m_base, n_base, e, lst);
         return;
       }
     }
@@ -720,7 +731,7 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
   float* ep = reinterpret_cast<float*>(smem) + wave * 32 * 68;
   if constexpr (EPI != EPI_GENERIC) {
     if (m0 + BBM <= M && n0 + BBN <= N) {
-      epilogue_fast<EPI>(acc, ep, lane, m_base, n_base, e, lst);
+      epilogue_fast<EPI, 32, DG>(acc, ep, lane, m_base, n_base, e, lst);
       return;
     }
   }
@@ -1131,6 +1142,53 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
     // mlp2 -1.5 %), LDS-staged row vectors for the others (attn_out -10 %, mlp3 -4 %)
     const bool tr = e.act != VTD_ACT_NONE;
     const dim3 g(tiles_m * tiles_n);
+#if VTD_DIAG
+    // epilogue ablation (wrong outputs): VTD_PP2_DG = the DG bits of epilogue_fast /
+    // epilogue_direct, for the plain / residual / statistics codes gemm_bench uses
+    static const int pp2_dg = getenv("VTD_PP2_DG") ? atoi(getenv("VTD_PP2_DG")) : 0;
+    if (pp2_dg > 0) {
+      bool done = true;
+      auto dg = [&](auto c) {
+        constexpr int C = decltype(c)::value;
+        static std::once_flag once[kMaxDevices];
+        once_per_device(once, [] {
+          for (const void* f : {reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, false, 1>),
+                                reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, true, 1>),
+                                reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, false, 2>),
+                                reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, true, 2>),
+                                reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, false, 4>),
+                                reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, true, 4>),
+                                reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, false, 8>),
+                                reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, true, 8>)})
+            (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
+        });
+#define VTD_DG_L(D)                                                                                \
+  if (pp2_dg == D) {                                                                               \
+    if (tr) hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, true, D>), g, dim3(BNT), 2 * BSTAGE,    \
+                               stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e, 1);       \
+    else hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, false, D>), g, dim3(BNT), 2 * BSTAGE,      \
+                            stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e, 1);          \
+  }
+        VTD_DG_L(1) VTD_DG_L(2) VTD_DG_L(4) VTD_DG_L(8)
+#undef VTD_DG_L
+      };
+      switch (code) {
+        case 4: dg(std::integral_constant<int, 4>{}); break;
+        case 5: dg(std::integral_constant<int, 5>{}); break;
+        case 12: dg(std::integral_constant<int, 12>{}); break;
+        case 13: dg(std::integral_constant<int, 13>{}); break;
+        case 12 | EPI_STAT: dg(std::integral_constant<int, 12 | EPI_STAT>{}); break;
+        case 13 | EPI_STAT: dg(std::integral_constant<int, 13 | EPI_STAT>{}); break;
+        case 4 | EPI_LNF: dg(std::integral_constant<int, 4 | EPI_LNF>{}); break;
+        case 5 | EPI_LNF: dg(std::integral_constant<int, 5 | EPI_LNF>{}); break;
+        default: done = false;
+      }
+      if (done) {
+        VTD_LAUNCH_CHECK("gemm");
+        return VTD_OK;
+      }
+    }
+#endif
     switch (code) {
 #define VTD_PP_CASE(C) \
   case C: pp2_launch<C>(tr, g, stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e); break;
