@@ -113,11 +113,13 @@ def test_gemm_bf16_output(L, cuda, dtype):
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("T", [196, 37, 1])
-def test_gemm_head_reshape_scatter(L, cuda, dtype, T):
+@pytest.mark.parametrize("K", [64, 768, 1024])
+def test_gemm_head_reshape_scatter(L, cuda, dtype, T, K):
     """Dense(17) + keras Reshape((17, -1)) (vtd.py:454-463) as a scatter epilogue:
-    must equal the row-major reinterpretation, NOT a transpose."""
+    must equal the row-major reinterpretation, NOT a transpose.
+    bf16 with K = 768 / 1024 takes the skinny (N <= 32) kernel."""
     code, tdt = _dt(L, dtype)
-    B, K = 3, 64
+    B = 3
     g = torch.Generator().manual_seed(T)
     A = torch.randn(B * T, K, generator=g).to(tdt)
     Bt = torch.randn(17, K, generator=g).to(tdt)
@@ -130,7 +132,7 @@ def test_gemm_head_reshape_scatter(L, cuda, dtype, T):
     t = (A.double() @ Bt.double().T + bias.double()).reshape(B, T, 17)
     u = t.reshape(B, 17, T)                     # row-major reshape
     got = out.cpu().double()[:, :T].reshape(B, 17, T)
-    assert (got - u).abs().max().item() < 1e-4
+    assert (got - u).abs().max().item() < 1e-4 * max(1.0, math.sqrt(K / 64))
     assert (out.cpu()[:, T:] == 0).all()
 
 

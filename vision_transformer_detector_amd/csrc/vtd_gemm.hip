@@ -144,6 +144,52 @@ __global__ __launch_bounds__(NT) void gemm_tn_kernel(
       }
 }
 
+// ============================================================================
+// Skinny bf16 GEMM, N <= 32 (the head's Dense(17) projection + Reshape scatter, vtd.py:454-463):
+// one wave computes 16 rows x 32 columns with v_mfma_f32_16x16x32_bf16.  Bt (32 x K, rows
+// past N zero) is staged once per 64-row workgroup in LDS, each row's 16-B chunk c at
+// position c ^ (row & 15) (the 16 rows of every ds_read_b128 lane group in 16 distinct bank
+// slots); A goes straight to registers, every K-step's load issued before the first MFMA.
+// The problem is memory-bound (A read once: 38.5 MB at C2, B = 256); the 128 x 128 kernel it
+// replaces ran 196 workgroups through 12 dependent register-staged K-steps.  K = 32 NKS.
+constexpr int SK_ROWS = 64;
+template <int NKS>
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(int M, int N, const bf16_t* __restrict__ A,
+                                                          int lda, const bf16_t* __restrict__ Bt,
+                                                          int ldb, EpiArgs e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KC = NKS * 4;                    // 16-B chunks per row
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, g = lane >> 4;
+  const int m0 = blockIdx.x * SK_ROWS + wave * 16;
+  const bf16_t* ap = A + (int64_t)min(m0 + fr, M - 1) * lda + 8 * g;
+  i32x4 a[NKS];
+#pragma unroll
+  for (int s = 0; s < NKS; ++s) a[s] = *reinterpret_cast<const i32x4*>(ap + s * 32);
+  for (int i = tid; i < 32 * KC; i += 256) {
+    const int r = i / KC, c = i - r * KC;
+    i32x4 v = {0, 0, 0, 0};
+    if (r < N) v = *reinterpret_cast<const i32x4*>(Bt + (int64_t)r * ldb + c * 8);
+    *reinterpret_cast<i32x4*>(smem + (r * KC + (c ^ (r & 15))) * 16) = v;
+  }
+  __syncthreads();
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int s = 0; s < NKS; ++s)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const int r = 16 * cb + fr, c = 4 * s + g;
+      const bf16x8 b = *reinterpret_cast<const bf16x8*>(smem + (r * KC + (c ^ (r & 15))) * 16);
+      acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[s]), b,
+                                                        acc[cb], 0, 0, 0);
+    }
+  // D layout: column 16 cb + fr, rows 4 g + r
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) epi_store(e, M, N, m0 + 4 * g + r, 16 * cb + fr, acc[cb][r]);
+}
+
 constexpr int BBM = 256, BBN = 256, BNT = 512;
 constexpr int BSTAGE = (BBM + BBN) * KB;     // 64 KiB per stage
 static_assert(8 * 32 * 68 * 4 <= 2 * BSTAGE, "epilogue staging must fit the stages");
@@ -1197,6 +1243,19 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
       default:
         pp2_launch<EPI_GENERIC>(tr, g, stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);
     }
+  } else if (dtype == VTD_BF16 && N <= 32 && (K == 512 || K == 768 || K == 1024)) {
+    const EpiArgs e = make_epi_args(epi);
+    const dim3 grid((M + SK_ROWS - 1) / SK_ROWS);
+    const size_t lds = (size_t)32 * K * 2;
+    if (K == 512) hipLaunchKernelGGL(gemm_skinny_kernel<16>, grid, dim3(256), lds, stream, M, N,
+                                     static_cast<const bf16_t*>(A), lda,
+                                     static_cast<const bf16_t*>(Bt), ldb, e);
+    else if (K == 768) hipLaunchKernelGGL(gemm_skinny_kernel<24>, grid, dim3(256), lds, stream, M, N,
+                                          static_cast<const bf16_t*>(A), lda,
+                                          static_cast<const bf16_t*>(Bt), ldb, e);
+    else hipLaunchKernelGGL(gemm_skinny_kernel<32>, grid, dim3(256), lds, stream, M, N,
+                            static_cast<const bf16_t*>(A), lda, static_cast<const bf16_t*>(Bt),
+                            ldb, e);
   } else {
     const EpiArgs e = make_epi_args(epi);
     dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM);
