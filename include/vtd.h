@@ -378,14 +378,17 @@ int vtd_profile_read(double* ms, int64_t* launches, double* flops, int n_classes
  *   VTD_KNOB_ATTN_GRID (VTD_ATTN_GRID): persistent attention workgroups (default: CUs).
  *   VTD_KNOB_GEMM_NGW (VTD_GEMM_NGW): GEMM tile-order group width (0 = row-major).
  *   VTD_KNOB_SPLITK (VTD_SPLITK): 0 disables the head's split-K (changes workspace size).
- *   VTD_KNOB_JPEG_CHUNK_BITS (VTD_JPEG_CHUNK_BITS): Huffman chunk length of vtd_jpeg_decode. */
+ *   VTD_KNOB_JPEG_CHUNK_BITS (VTD_JPEG_CHUNK_BITS): Huffman chunk length of vtd_jpeg_decode.
+ *   VTD_KNOB_SKINNY (VTD_SKINNY): 0 keeps the head's narrow bf16 layers (N <= 320) on the
+ *     128 x 128 kernel instead of the skinny one. */
 enum {
   VTD_KNOB_ATTN_VARIANT = 0,
   VTD_KNOB_ATTN_GRID = 1,
   VTD_KNOB_GEMM_NGW = 2,
   VTD_KNOB_SPLITK = 3,
   VTD_KNOB_JPEG_CHUNK_BITS = 4,
-  VTD_KNOB_COUNT = 5
+  VTD_KNOB_SKINNY = 5,
+  VTD_KNOB_COUNT = 6
 };
 int vtd_set_knob(int knob, int value);
 int vtd_get_knob(int knob);

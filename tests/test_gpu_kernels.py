@@ -111,6 +111,38 @@ def test_gemm_bf16_output(L, cuda, dtype):
     assert rel < 8e-3     # one bf16 rounding of the output (2^-8)
 
 
+@pytest.mark.parametrize("M,N,K,act,out_dtype,resid", [
+    (2176, 320, 576, 2, 1, False),     # the head's Dense(272) per C2 micro-batch, mish
+    (2176, 192, 320, 1, 1, False),     # Dense(136), gelu
+    (2176, 6, 192, 0, 0, False),       # MLP_Head_no_Sigmoid
+    (25088, 17, 768, 0, 1, False),     # Dense(17) (without the scatter)
+    (1000, 100, 2048, 1, 0, True),     # the largest K, ragged M and N, f32 residual
+    (33, 64, 64, 2, 1, True),          # one K-step pair, bf16 residual in place
+    (777, 257, 1088, 0, 0, False)])    # ragged column block
+@pytest.mark.parametrize("skinny", [1, 0])
+def test_gemm_skinny(L, cuda, M, N, K, act, out_dtype, resid, skinny):
+    """The skinny bf16 kernel (N <= 320, below the 256-tile threshold) against fp64, and the
+    128 x 128 kernel it replaces (knob VTD_KNOB_SKINNY = 0): both fp32 accumulation of bf16
+    products, so they agree to fp32 summation order."""
+    g = torch.Generator(device=cuda).manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
+    Bt = (torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g, device=cuda)
+    odt = torch.float32 if out_dtype == 0 else torch.bfloat16
+    out = torch.randn(M, N, generator=g, device=cuda).to(odt)
+    x0 = out.clone()
+    with L.knob(L.KNOB_SKINNY, skinny):
+        _gemm(L, A, Bt, L.BF16, bias=bias, act=act, resid=out if resid else None, out=out,
+              out_dtype=out_dtype)
+    ref64 = _np_act(act, (A.double() @ Bt.double().T + bias.double()).cpu().numpy())
+    if resid:
+        ref64 = ref64 + x0.double().cpu().numpy()
+    got = out.double().cpu().numpy()
+    tol = 2e-5 if out_dtype == 0 else 8e-3
+    err = np.abs(got - ref64) / np.maximum(np.abs(ref64), 1.0)
+    assert err.max() < tol, (err.max(), np.argwhere(err >= tol)[:5].tolist())
+
+
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("T", [196, 37, 1])
 @pytest.mark.parametrize("K", [64, 768, 1024])

@@ -145,49 +145,69 @@ __global__ __launch_bounds__(NT) void gemm_tn_kernel(
 }
 
 // ============================================================================
-// Skinny bf16 GEMM, N <= 32 (the head's Dense(17) projection + Reshape scatter, vtd.py:454-463):
-// one wave computes 16 rows x 32 columns with v_mfma_f32_16x16x32_bf16.  Bt (32 x K, rows
-// past N zero) is staged once per 64-row workgroup in LDS, each row's 16-B chunk c at
-// position c ^ (row & 15) (the 16 rows of every ds_read_b128 lane group in 16 distinct bank
-// slots); A goes straight to registers, every K-step's load issued before the first MFMA.
-// The problem is memory-bound (A read once: 38.5 MB at C2, B = 256); the 128 x 128 kernel it
-// replaces ran 196 workgroups through 12 dependent register-staged K-steps.  K = 32 NKS.
-constexpr int SK_ROWS = 64;
-template <int NKS>
-__global__ __launch_bounds__(256) void gemm_skinny_kernel(int M, int N, const bf16_t* __restrict__ A,
-                                                          int lda, const bf16_t* __restrict__ Bt,
-                                                          int ldb, EpiArgs e) {
+// Skinny bf16 GEMM for the detection head's narrow layers at B x 17 rows and its Dense(17)
+// projection (vtd.py:454-493): a 256-thread workgroup computes 64 rows x 32 columns, one
+// wave 16 rows x 32 columns with v_mfma_f32_16x16x32_bf16.  The workgroup's 32 rows of Bt
+// (rows past N zero) are staged once in LDS as the GEMM's 128-B-row image per 64-wide K slab
+// (chunk ^ (row & 7): conflict-free ds_read_b128 B reads); A goes straight to registers in
+// chunks of SK_CH K-steps, the next chunk's loads in flight while one is multiplied.  These
+// layers are latency-bound: the 128 x 128 kernel ran 17-51 workgroups per layer through
+// dependent register-staged K-steps, the 256-tile kernel needs >= 128 tiles.
+// K % 64 == 0, K <= SK_KMAX.
+constexpr int SK_ROWS = 64, SK_CH = 8, SK_KMAX = 2048;
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(int M, int N, int K,
+                                                          const bf16_t* __restrict__ A, int lda,
+                                                          const bf16_t* __restrict__ Bt, int ldb,
+                                                          EpiArgs e) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int KC = NKS * 4;                    // 16-B chunks per row
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, g = lane >> 4;
-  const int m0 = blockIdx.x * SK_ROWS + wave * 16;
+  const int m0 = blockIdx.x * SK_ROWS + wave * 16, n0 = blockIdx.y * 32;
+  const int nks = K >> 5;                         // 32-wide K-steps
   const bf16_t* ap = A + (int64_t)min(m0 + fr, M - 1) * lda + 8 * g;
-  i32x4 a[NKS];
+  i32x4 a0[SK_CH], a1[SK_CH];
+  auto load = [&](i32x4 (&a)[SK_CH], int s0) {
 #pragma unroll
-  for (int s = 0; s < NKS; ++s) a[s] = *reinterpret_cast<const i32x4*>(ap + s * 32);
-  for (int i = tid; i < 32 * KC; i += 256) {
-    const int r = i / KC, c = i - r * KC;
+    for (int j = 0; j < SK_CH; ++j)   // past the end: re-read the last step (no branches)
+      a[j] = *reinterpret_cast<const i32x4*>(ap + min(s0 + j, nks - 1) * 32);
+  };
+  load(a0, 0);
+  // Bt rows n0 .. n0 + 31: slab t = k / 64, row r, 16-B chunk c at t * 4096 + r * 128 + (c ^ (r & 7)) * 16
+  for (int i = tid; i < 32 * (K >> 3); i += 256) {
+    const int r = i / (K >> 3), cc = i - r * (K >> 3), t = cc >> 3, c = cc & 7;
     i32x4 v = {0, 0, 0, 0};
-    if (r < N) v = *reinterpret_cast<const i32x4*>(Bt + (int64_t)r * ldb + c * 8);
-    *reinterpret_cast<i32x4*>(smem + (r * KC + (c ^ (r & 15))) * 16) = v;
+    if (n0 + r < N) v = *reinterpret_cast<const i32x4*>(Bt + (int64_t)(n0 + r) * ldb + cc * 8);
+    *reinterpret_cast<i32x4*>(smem + t * 4096 + r * 128 + ((c ^ (r & 7)) << 4)) = v;
   }
   __syncthreads();
   f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  auto compute = [&](const i32x4 (&a)[SK_CH], int s0) {
 #pragma unroll
-  for (int s = 0; s < NKS; ++s)
+    for (int j = 0; j < SK_CH; ++j) {
+      const int st = s0 + j;
+      if (st < nks) {
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      const int r = 16 * cb + fr, c = 4 * s + g;
-      const bf16x8 b = *reinterpret_cast<const bf16x8*>(smem + (r * KC + (c ^ (r & 15))) * 16);
-      acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[s]), b,
-                                                        acc[cb], 0, 0, 0);
+        for (int cb = 0; cb < 2; ++cb) {
+          const int r = 16 * cb + fr, c = 4 * (st & 1) + g;
+          const bf16x8 b = *reinterpret_cast<const bf16x8*>(smem + (st >> 1) * 4096 + r * 128 +
+                                                            ((c ^ (r & 7)) << 4));
+          acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[j]), b,
+                                                            acc[cb], 0, 0, 0);
+        }
+      }
     }
-  // D layout: column 16 cb + fr, rows 4 g + r
+  };
+  for (int s0 = 0; s0 < nks; s0 += 2 * SK_CH) {
+    if (s0 + SK_CH < nks) load(a1, s0 + SK_CH);
+    compute(a0, s0);
+    if (s0 + 2 * SK_CH < nks) load(a0, s0 + 2 * SK_CH);
+    if (s0 + SK_CH < nks) compute(a1, s0 + SK_CH);
+  }
+  // D layout: column n0 + 16 cb + fr, rows 4 g + r
 #pragma unroll
   for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) epi_store(e, M, N, m0 + 4 * g + r, 16 * cb + fr, acc[cb][r]);
+    for (int r = 0; r < 4; ++r) epi_store(e, M, N, m0 + 4 * g + r, n0 + 16 * cb + fr, acc[cb][r]);
 }
 
 constexpr int BBM = 256, BBN = 256, BNT = 512;
@@ -1072,6 +1092,14 @@ bool gemm_emits_stats(int M, int N, int dtype, const vtd_epilogue* e) {
   return (pp2_code(e) & EPI_STAT) != 0 && pp2_code(e) != EPI_GENERIC;
 }
 
+// The skinny kernel for problems the 256-tile kernels do not take (< kMinBigTiles tiles or
+// N <= 64): the head's Dense(17) projection (any M) and its narrow layers, when every
+// 32-column block re-reads A at most 10 times (N <= 320) -- wider layers keep the 128 x 128
+// kernel's A reuse.  VTD_KNOB_SKINNY = 0 disables it.
+bool skinny_choice(int M, int N, int K) {
+  return knob(VTD_KNOB_SKINNY) != 0 && N <= 320 && K % 64 == 0 && M > 0;
+}
+
 // Whether vtd_gemm_mx8 can write its output as MX-fp8 (out_dtype VTD_FP8): the fast
 // epilogue on every tile, no residual or rare modes.
 bool gemm_mx8_emits_fp8(int M, int N, const vtd_epilogue* e) {
@@ -1243,19 +1271,17 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
       default:
         pp2_launch<EPI_GENERIC>(tr, g, stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);
     }
-  } else if (dtype == VTD_BF16 && N <= 32 && (K == 512 || K == 768 || K == 1024)) {
+  } else if (dtype == VTD_BF16 && K <= SK_KMAX && skinny_choice(M, N, K)) {
     const EpiArgs e = make_epi_args(epi);
-    const dim3 grid((M + SK_ROWS - 1) / SK_ROWS);
+    const dim3 grid((M + SK_ROWS - 1) / SK_ROWS, (N + 31) / 32);
     const size_t lds = (size_t)32 * K * 2;
-    if (K == 512) hipLaunchKernelGGL(gemm_skinny_kernel<16>, grid, dim3(256), lds, stream, M, N,
-                                     static_cast<const bf16_t*>(A), lda,
-                                     static_cast<const bf16_t*>(Bt), ldb, e);
-    else if (K == 768) hipLaunchKernelGGL(gemm_skinny_kernel<24>, grid, dim3(256), lds, stream, M, N,
-                                          static_cast<const bf16_t*>(A), lda,
-                                          static_cast<const bf16_t*>(Bt), ldb, e);
-    else hipLaunchKernelGGL(gemm_skinny_kernel<32>, grid, dim3(256), lds, stream, M, N,
-                            static_cast<const bf16_t*>(A), lda, static_cast<const bf16_t*>(Bt),
-                            ldb, e);
+    static std::once_flag once[kMaxDevices];
+    once_per_device(once, [] {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_skinny_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 32 * SK_KMAX * 2);
+    });
+    hipLaunchKernelGGL(gemm_skinny_kernel, grid, dim3(256), lds, stream, M, N, K,
+                       static_cast<const bf16_t*>(A), lda, static_cast<const bf16_t*>(Bt), ldb, e);
   } else {
     const EpiArgs e = make_epi_args(epi);
     dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM);
