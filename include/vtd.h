@@ -380,7 +380,9 @@ int vtd_profile_read(double* ms, int64_t* launches, double* flops, int n_classes
  *   VTD_KNOB_SPLITK (VTD_SPLITK): 0 disables the head's split-K (changes workspace size).
  *   VTD_KNOB_JPEG_CHUNK_BITS (VTD_JPEG_CHUNK_BITS): Huffman chunk length of vtd_jpeg_decode.
  *   VTD_KNOB_SKINNY (VTD_SKINNY): 0 keeps the head's narrow bf16 layers (N <= 320) on the
- *     128 x 128 kernel instead of the skinny one. */
+ *     128 x 128 kernel instead of the skinny one.
+ *   VTD_KNOB_F32_PP2 (VTD_F32_PP2): 0 keeps large fp32-mode GEMMs on the 128 x 128 kernel
+ *     instead of the 256-tile f32 one. */
 enum {
   VTD_KNOB_ATTN_VARIANT = 0,
   VTD_KNOB_ATTN_GRID = 1,
@@ -388,7 +390,8 @@ enum {
   VTD_KNOB_SPLITK = 3,
   VTD_KNOB_JPEG_CHUNK_BITS = 4,
   VTD_KNOB_SKINNY = 5,
-  VTD_KNOB_COUNT = 6
+  VTD_KNOB_F32_PP2 = 6,
+  VTD_KNOB_COUNT = 7
 };
 int vtd_set_knob(int knob, int value);
 int vtd_get_knob(int knob);

@@ -376,6 +376,35 @@ def test_gemm_bf16_256_tile_path(L, cuda, M, N, K, act, out_dtype):
 
 
 @pytest.mark.parametrize("M,N,K,act,resid", [
+    (12544, 2304, 768, 0, False),    # the fp32 mode's query/key/value at C2 B = 64
+    (6272, 3072, 768, 1, False),     # mlp1 (gelu), transposed-accumulator epilogue
+    (12544, 768, 1536, 2, True),     # mish + f32 residual in place
+    (4100, 2100, 192, 0, True),      # ragged M / N: generic epilogue on the split tiles
+    (4096, 4096, 64, 1, False)])     # one K-step pair
+def test_gemm_f32_256_tile_path(L, cuda, M, N, K, act, resid):
+    """The fp32 parity mode's 256-tile kernel (v_mfma_f32_16x16x4_f32, exact fp32 fma
+    chains) against fp64 and against the 128 x 128 kernel (knob VTD_KNOB_F32_PP2 = 0)."""
+    g = torch.Generator(device=cuda).manual_seed(M + N + K + act)
+    A = torch.randn(M, K, generator=g, device=cuda)
+    Bt = torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)
+    bias = torch.randn(N, generator=g, device=cuda)
+    x0 = torch.randn(M, N, generator=g, device=cuda)
+    outs = {}
+    for v in (1, 0):
+        x = x0.clone()
+        with L.knob(L.KNOB_F32_PP2, v):
+            _gemm(L, A, Bt, L.F32, bias=bias, act=act, resid=x if resid else None, out=x,
+                  out_dtype=0)
+        outs[v] = x
+    ref64 = _np_act(act, (A.double() @ Bt.double().T + bias.double()).cpu().numpy())
+    if resid:
+        ref64 = ref64 + x0.double().cpu().numpy()
+    for v, x in outs.items():
+        err = np.abs(x.double().cpu().numpy() - ref64) / np.maximum(np.abs(ref64), 1.0)
+        assert err.max() < 2e-5, (v, err.max(), np.argwhere(err >= 2e-5)[:5].tolist())
+
+
+@pytest.mark.parametrize("M,N,K,act,resid", [
     (50176, 768, 768, 0, True),      # attn_out at C2 B=256: 588 tiles = 2.3 rounds
     (50176, 768, 1536, 1, True),     # mlp3
     (12544, 1536, 3072, 1, False),   # mlp2 at B=64: 294 tiles

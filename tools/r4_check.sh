@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out/r4b
 timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_model.py::test_single_layer_mlp_fold_full_tiles tests/test_gpu_model.py::test_concurrent_split_forwards_on_two_streams tests/test_gpu_kernels.py::test_gemm_statout_needs_a_specialised_epilogue > gpurun_out/r4b/new_tests.log 2>&1 || { tail -40 gpurun_out/r4b/new_tests.log; exit 1; }
 tail -3 gpurun_out/r4b/new_tests.log
-timeout -k 10 300 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_kernels.py -k "attention or reshape_scatter or skinny" > gpurun_out/r4b/attn_tests.log 2>&1 || { tail -40 gpurun_out/r4b/attn_tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_kernels.py -k "attention or reshape_scatter or skinny or f32_256" > gpurun_out/r4b/attn_tests.log 2>&1 || { tail -40 gpurun_out/r4b/attn_tests.log; exit 1; }
 tail -1 gpurun_out/r4b/attn_tests.log
 timeout -k 10 200 python tools/attn_bench.py --variants 4,5 --rounds 3 > gpurun_out/r4b/attn_ab.jsonl 2>&1 || { tail -20 gpurun_out/r4b/attn_ab.jsonl; exit 1; }
 cat gpurun_out/r4b/attn_ab.jsonl

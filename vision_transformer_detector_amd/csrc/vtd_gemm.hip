@@ -400,18 +400,37 @@ __device__ __forceinline__ void pp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int I0, int J0>
+// F32: the fp32 parity mode's operands (a 16-B fragment = 4 f32 K-elements): four
+// v_mfma_f32_16x16x4_f32 per fragment pair (exact fp32 fma chain), the K-element t of lane
+// group fg being K index 4 (4 s + fg) + t of the 32-wide K-step -- the same LDS image and
+// reads as bf16, four times the MFMAs per byte.  Consecutive MFMAs hit different accumulators
+// (the f32 MFMA's dependent latency exceeds its issue time).
+template <int I0, int J0, bool F32 = false>
 __device__ __forceinline__ void pp_mfma(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][2],
                                         const bf16x8 (&b)[2][2]) {
   __builtin_amdgcn_s_setprio(1);
+  if constexpr (F32) {
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[I0 + i][J0 + j] =
-            __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s], b[j][s], acc[I0 + i][J0 + j], 0, 0, 0);
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[I0 + i][J0 + j] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                __builtin_bit_cast(f32x4, a[i][s])[t], __builtin_bit_cast(f32x4, b[j][s])[t],
+                acc[I0 + i][J0 + j], 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[I0 + i][J0 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s], b[j][s], acc[I0 + i][J0 + j], 0, 0, 0);
+  }
   __builtin_amdgcn_s_setprio(0);
 }
 
@@ -455,18 +474,32 @@ __device__ __forceinline__ void pp_load_b_t(bf16x8 (&b)[2][2], const char* lb, i
       b[j][s] = *reinterpret_cast<const bf16x8*>(lb + swz_t(row0 + perm_t(j, fr), 4 * s + fg));
 }
 
-template <int I0, int J0>
+template <int I0, int J0, bool F32 = false>
 __device__ __forceinline__ void pp_mfma_t(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][2],
                                           const bf16x8 (&b)[2][2]) {
   __builtin_amdgcn_s_setprio(1);
+  if constexpr (F32) {
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[I0 + i][J0 + j] =
-            __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][s], a[i][s], acc[I0 + i][J0 + j], 0, 0, 0);
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[I0 + i][J0 + j] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                __builtin_bit_cast(f32x4, b[j][s])[t], __builtin_bit_cast(f32x4, a[i][s])[t],
+                acc[I0 + i][J0 + j], 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[I0 + i][J0 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][s], a[i][s], acc[I0 + i][J0 + j], 0, 0, 0);
+  }
   __builtin_amdgcn_s_setprio(0);
 }
 
@@ -500,18 +533,19 @@ struct PP2BufSrc {
   int off[4][2];
 };
 
-template <bool TR>
-__device__ __forceinline__ void pp2b_sources(PP2BufSrc& s, const bf16_t* A, int lda, int M,
-                                             const bf16_t* Bt, int ldb, int N, int m0, int n0,
+template <bool TR, typename T = bf16_t>
+__device__ __forceinline__ void pp2b_sources(PP2BufSrc& s, const T* A, int lda, int M,
+                                             const T* Bt, int ldb, int N, int m0, int n0,
                                              int wave, int lane, int k0 = 0) {
   // records = bytes from the tile base to the end of the operand (clamped to 32 bits); all
   // offsets are in range because rows are clamped to the last valid row.  k0: first K
-  // element of the loop (stream-K segments), folded into the base.
-  const int64_t ra_bytes = (int64_t)(M - m0) * lda * 2 - 2 * k0,
-                rb_bytes = (int64_t)(N - n0) * ldb * 2 - 2 * k0;
-  s.ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(A + (int64_t)m0 * lda + k0), 0,
+  // element of the loop (split-K ranges), folded into the base.
+  constexpr int ES = (int)sizeof(T);
+  const int64_t ra_bytes = (int64_t)(M - m0) * lda * ES - ES * k0,
+                rb_bytes = (int64_t)(N - n0) * ldb * ES - ES * k0;
+  s.ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(A + (int64_t)m0 * lda + k0), 0,
                                            (int)std::min<int64_t>(ra_bytes, 0x7fffffff), 0x00020000);
-  s.rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(Bt + (int64_t)n0 * ldb + k0), 0,
+  s.rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(Bt + (int64_t)n0 * ldb + k0), 0,
                                            (int)std::min<int64_t>(rb_bytes, 0x7fffffff), 0x00020000);
   const int prow = lane >> 3, pchunk = (lane & 7) ^ prow;
 #pragma unroll
@@ -521,8 +555,8 @@ __device__ __forceinline__ void pp2b_sources(PP2BufSrc& s, const bf16_t* A, int 
       const int tr = grp_tile_row(g, (wave * 2 + j) * 8 + prow);
       // transposed variant: B groups use swz_t (group row bit 4 = wave & 1 flips chunk bit 2)
       const int bchunk = TR ? pchunk ^ ((wave & 1) << 2) : pchunk;
-      s.off[g][j] = g < 2 ? min(tr, M - 1 - m0) * lda * 2 + pchunk * 16
-                          : min(tr, N - 1 - n0) * ldb * 2 + bchunk * 16;
+      s.off[g][j] = g < 2 ? min(tr, M - 1 - m0) * lda * ES + pchunk * 16
+                          : min(tr, N - 1 - n0) * ldb * ES + bchunk * 16;
     }
 }
 
@@ -537,7 +571,7 @@ __device__ __forceinline__ void pp2_issue(char* smem, const PP2BufSrc& src, int 
                                              kt * 128, 0, 0);
 }
 
-template <bool TR>
+template <bool TR, bool F32 = false>
 __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, const PP2BufSrc& src,
                                              int nk, int wave, int wm, int wn, int fr, int fg) {
   // prologue: tile 0 complete, tile 1's X0/Y0/Y1 in flight
@@ -570,8 +604,8 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
     if constexpr (n1) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     pp_barrier();
-    if constexpr (TR) pp_mfma_t<0, 0>(acc, a, b0);
-    else pp_mfma<0, 0>(acc, a, b0);
+    if constexpr (TR) pp_mfma_t<0, 0, F32>(acc, a, b0);
+    else pp_mfma<0, 0, F32>(acc, a, b0);
     pp_barrier();
     // ---- P1
     if constexpr (TR) pp_load_b_t(b1, st + 3 * 16384, rb, fr, fg);
@@ -579,15 +613,15 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
     if constexpr (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     pp_barrier();
-    if constexpr (TR) pp_mfma_t<0, 2>(acc, a, b1);
-    else pp_mfma<0, 2>(acc, a, b1);
+    if constexpr (TR) pp_mfma_t<0, 2, F32>(acc, a, b1);
+    else pp_mfma<0, 2, F32>(acc, a, b1);
     pp_barrier();
     // ---- P2
     pp_load_a(a, st + 1 * 16384, ra, fr, fg);
     if constexpr (n2) pp2_issue<0>(smem, src, wave, kt + 2, kt & 1);
     pp_barrier();
-    if constexpr (TR) pp_mfma_t<4, 2>(acc, a, b1);
-    else pp_mfma<4, 2>(acc, a, b1);
+    if constexpr (TR) pp_mfma_t<4, 2, F32>(acc, a, b1);
+    else pp_mfma<4, 2, F32>(acc, a, b1);
     pp_barrier();
     // ---- P3
     if constexpr (n2) {
@@ -598,8 +632,8 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     pp_barrier();
-    if constexpr (TR) pp_mfma_t<4, 0>(acc, a, b0);
-    else pp_mfma<4, 0>(acc, a, b0);
+    if constexpr (TR) pp_mfma_t<4, 0, F32>(acc, a, b0);
+    else pp_mfma<4, 0, F32>(acc, a, b0);
     pp_barrier();
   };
   int kt = 0;
@@ -798,6 +832,57 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
   if constexpr (EPI != EPI_GENERIC) {
     if (m0 + BBM <= M && n0 + BBN <= N) {
       epilogue_fast<EPI, 32, DG>(acc, ep, lane, m_base, n_base, e, lst);
+      return;
+    }
+  }
+  epilogue_generic(acc, ep, lane, M, N, m_base, n_base, e);
+}
+
+// The fp32 parity mode's 256 x 256-tile kernel: pp2's staging, ping-pong schedule and
+// epilogues with f32 operands (a 128-B K-step row = 32 f32) on v_mfma_f32_16x16x4_f32
+// (pp_mfma<.., true>).  MFMA-bound: a K-step's 64 KiB of operands feed 16x the MFMA cycles
+// of the bf16 kernel's.
+template <int EPI, bool TR>
+__global__ __launch_bounds__(BNT) void gemm_tn_f32_pp2_kernel(
+    int M, int N, int K, const float* __restrict__ A, int lda, const float* __restrict__ Bt,
+    int ldb, int tiles_m, int tiles_n, EpiArgs e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nt = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nt >> 3, r = nt & 7;
+  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  int tm, tn;
+  tile_coords(tile, tiles_m, tiles_n, e.ngw, tm, tn);
+  const int m0 = tm * BBM, n0 = tn * BBN;
+  PP2BufSrc src;
+  pp2b_sources<TR, float>(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane, 0);
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fg = lane >> 4;
+  pp2_mainloop<TR, true>(acc, smem, src, K / 32, wave, wm, wn, fr, fg);
+  const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
+  if constexpr (TR) {
+    if constexpr (EPI != EPI_GENERIC) {
+      if (m0 + BBM <= M && n0 + BBN <= N) {
+        epilogue_direct<EPI>(acc, lane, m_base, n_base, e);
+        return;
+      }
+    }
+    epilogue_direct_generic(acc, reinterpret_cast<float*>(smem) + wave * 32 * 68, lane, M, N,
+                            m_base, n_base, e);
+    return;
+  }
+  float* ep = reinterpret_cast<float*>(smem) + wave * 32 * 68;
+  if constexpr (EPI != EPI_GENERIC) {
+    if (m0 + BBM <= M && n0 + BBN <= N) {
+      epilogue_fast<EPI>(acc, ep, lane, m_base, n_base, e);
       return;
     }
   }
@@ -1157,6 +1242,50 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
                    int dtype, const vtd_epilogue* epi, hipStream_t stream, double flops,
                    const float* lnpart, int lnslots, int lnD, float lneps);
 
+// the f32 256-tile kernel: the f32-output codes the fp32 mode's forward uses (bias,
+// activation, f32 residual, the position-embedding row add); anything else generic
+#define VTD_F32_CODES(X) X(0) X(1) X(2) X(8) X(9) X(10) X(EPI_RA)
+void f32_pp2_launch(int M, int N, int K, const float* A, int lda, const float* Bt, int ldb,
+                    const vtd_epilogue* epi, int tiles_m, int tiles_n, hipStream_t stream) {
+  static std::once_flag once[kMaxDevices];
+  once_per_device(once, [] {
+#define VTD_F32_FN(C) reinterpret_cast<const void*>(&gemm_tn_f32_pp2_kernel<C, false>), \
+                      reinterpret_cast<const void*>(&gemm_tn_f32_pp2_kernel<C, true>),
+    const void* fns[] = {VTD_F32_FN(EPI_GENERIC) VTD_F32_CODES(VTD_F32_FN)};
+#undef VTD_F32_FN
+    for (const void* f : fns)
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
+  });
+  EpiArgs e = make_epi_args(epi);
+  e.ngw = tile_group_width(tiles_n);
+  int code = EPI_GENERIC;
+  if (pp2_fast_epilogue(epi) && epi->out_dtype == VTD_F32 && !epi->lnstat && !epi->statout &&
+      !epi->out2) {
+    const int c = epi_code(e.act, false, e.resid != nullptr) | (e.rowadd ? EPI_RA : 0);
+#define VTD_F32_IS(C) c == (C) ||
+    if (VTD_F32_CODES(VTD_F32_IS) false) code = c;
+#undef VTD_F32_IS
+  }
+  const bool tr = e.act != VTD_ACT_NONE;
+  const dim3 g(tiles_m * tiles_n);
+  switch (code) {
+#define VTD_F32_CASE(C)                                                                         \
+  case C:                                                                                       \
+    if (tr) hipLaunchKernelGGL((gemm_tn_f32_pp2_kernel<C, true>), g, dim3(BNT), 2 * BSTAGE,     \
+                               stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);          \
+    else hipLaunchKernelGGL((gemm_tn_f32_pp2_kernel<C, false>), g, dim3(BNT), 2 * BSTAGE,       \
+                            stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);             \
+    break;
+    VTD_F32_CODES(VTD_F32_CASE)
+#undef VTD_F32_CASE
+    default:
+      if (tr) hipLaunchKernelGGL((gemm_tn_f32_pp2_kernel<EPI_GENERIC, true>), g, dim3(BNT),
+                                 2 * BSTAGE, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
+      else hipLaunchKernelGGL((gemm_tn_f32_pp2_kernel<EPI_GENERIC, false>), g, dim3(BNT),
+                              2 * BSTAGE, stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
+  }
+}
+
 int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
                 int dtype, const vtd_epilogue* epi, hipStream_t stream, double flops) {
   return gemm_launch_ln(M, N, K, A, lda, Bt, ldb, dtype, epi, stream, flops, nullptr, 0, 0, 0.f);
@@ -1271,6 +1400,10 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
       default:
         pp2_launch<EPI_GENERIC>(tr, g, stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);
     }
+  } else if (dtype == VTD_F32 && tiles_m * tiles_n >= kMinBigTiles && N > 64 &&
+             knob(VTD_KNOB_F32_PP2) != 0) {
+    f32_pp2_launch(M, N, K, static_cast<const float*>(A), lda, static_cast<const float*>(Bt), ldb,
+                   epi, tiles_m, tiles_n, stream);
   } else if (dtype == VTD_BF16 && K <= SK_KMAX && skinny_choice(M, N, K)) {
     const EpiArgs e = make_epi_args(epi);
     const dim3 grid((M + SK_ROWS - 1) / SK_ROWS, (N + 31) / 32);
