@@ -382,7 +382,9 @@ int vtd_profile_read(double* ms, int64_t* launches, double* flops, int n_classes
  *   VTD_KNOB_SKINNY (VTD_SKINNY): 0 keeps the head's narrow bf16 layers (N <= 320) on the
  *     128 x 128 kernel instead of the skinny one.
  *   VTD_KNOB_F32_PP2 (VTD_F32_PP2): 0 keeps large fp32-mode GEMMs on the 128 x 128 kernel
- *     instead of the 256-tile f32 one. */
+ *     instead of the 256-tile f32 one.
+ *   VTD_KNOB_STAGGER (VTD_STAGGER): the two-stream split's second micro-batch starts k stages
+ *     (patch embedding, encoder layers) behind the first (default 0: in phase). */
 enum {
   VTD_KNOB_ATTN_VARIANT = 0,
   VTD_KNOB_ATTN_GRID = 1,
@@ -391,7 +393,8 @@ enum {
   VTD_KNOB_JPEG_CHUNK_BITS = 4,
   VTD_KNOB_SKINNY = 5,
   VTD_KNOB_F32_PP2 = 6,
-  VTD_KNOB_COUNT = 7
+  VTD_KNOB_STAGGER = 7,
+  VTD_KNOB_COUNT = 8
 };
 int vtd_set_knob(int knob, int value);
 int vtd_get_knob(int knob);

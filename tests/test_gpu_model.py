@@ -202,6 +202,21 @@ def test_two_stream_split_matches_single_images(vtd, cuda, dtype):
             assert ok, (i, rel)
 
 
+@pytest.mark.parametrize("stagger", [1, 3])
+def test_two_stream_split_stagger_is_bit_exact(vtd, cuda, stagger):
+    """Knob VTD_KNOB_STAGGER: the second micro-batch `stagger` stages behind the first
+    changes only when kernels run, never what they compute."""
+    from vision_transformer_detector_amd import _lib as L
+    model = vtd.create_vision_transformer_detector(**SPLIT_KW, dtype="bfloat16", seed=5)
+    g = torch.Generator(device=cuda).manual_seed(3)
+    x = torch.rand(128, 224, 224, 3, generator=g, device=cuda) * 2 - 1
+    ref = model(x).clone()
+    with L.knob(L.KNOB_STAGGER, stagger):
+        got = model(x)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+
+
 def test_two_stream_split_graph_capture(vtd, cuda):
     """The split forward (fork / join events to the internal stream) is HIP-graph
     capturable: the replay reproduces the eager result exactly."""

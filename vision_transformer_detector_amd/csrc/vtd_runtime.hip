@@ -59,7 +59,7 @@ namespace {
 constexpr const char* kKnobEnv[VTD_KNOB_COUNT] = {"VTD_ATTN_VARIANT", "VTD_ATTN_GRID",
                                                   "VTD_GEMM_NGW", "VTD_SPLITK",
                                                   "VTD_JPEG_CHUNK_BITS", "VTD_SKINNY",
-                                                  "VTD_F32_PP2"};
+                                                  "VTD_F32_PP2", "VTD_STAGGER"};
 std::atomic<int> g_knob[VTD_KNOB_COUNT];
 std::once_flag g_knob_once;
 void knob_init() {
@@ -413,10 +413,16 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
   // one caller at a time per device from the fork record to the join wait (SideStream)
   std::unique_lock<std::mutex> side_lock;
   if (side) side_lock = std::unique_lock<std::mutex>(side->mu);
-  if (side) {                       // fork: one record, every side stream waits on it
+  // fork: one record, every side stream waits on it.  Knob VTD_KNOB_STAGGER = k > 0: the
+  // record follows the caller-stream part's first k stages, so the other parts run k
+  // stages behind (their kernels then pair with different kernels of the first part)
+  const int stagger = side ? std::min(std::max(knob(VTD_KNOB_STAGGER), 0), n_stages) : 0;
+  auto fork = [&]() -> int {
     VTD_HIP(hipEventRecord(side->fork, st));
     for (int part = 1; part < ns; ++part) VTD_HIP(hipStreamWaitEvent(side->s[part - 1], side->fork, 0));
-  }
+    return VTD_OK;
+  };
+  if (side && stagger == 0 && (rc = fork())) return rc;
   struct Part {
     vtd_config cfg;
     const float* images;
@@ -447,9 +453,12 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
   // Launches are interleaved part by part, one stage (encoder layer) at a time: issuing
   // all of one part's ~110 launches before the next part's first one left the second
   // stream idle for the host's whole enqueue time of the first (~0.7 ms at C2, B = 256).
-  for (int s = 0; s < n_stages; ++s)
+  for (int t = 0; t < n_stages + stagger; ++t)
     for (int part = 0; part < ns; ++part) {
       Part& P = parts[part];
+      const int s = part == 0 ? t : t - stagger;
+      if (part == 1 && t == stagger && stagger > 0 && (rc = fork())) return rc;
+      if (s < 0 || s >= n_stages) continue;
       rc = forward_impl(&P.cfg, w, P.images, P.logits, P.dets, P.ws, P.st, s, s + 1, P.partials);
       if (rc) return rc;
     }
