@@ -384,7 +384,9 @@ int vtd_profile_read(double* ms, int64_t* launches, double* flops, int n_classes
  *   VTD_KNOB_F32_PP2 (VTD_F32_PP2): 0 keeps large fp32-mode GEMMs on the 128 x 128 kernel
  *     instead of the 256-tile f32 one.
  *   VTD_KNOB_STAGGER (VTD_STAGGER): the two-stream split's second micro-batch starts k stages
- *     (patch embedding, encoder layers) behind the first (default 0: in phase). */
+ *     (patch embedding, encoder layers) behind the first (default 0: in phase).
+ *   VTD_KNOB_GEMM_TR (VTD_GEMM_TR): 256-tile bf16 GEMM accumulator layout, 1 = transposed
+ *     (register-direct epilogue) for every layer, 0 = for none (default: activation layers). */
 enum {
   VTD_KNOB_ATTN_VARIANT = 0,
   VTD_KNOB_ATTN_GRID = 1,
@@ -394,7 +396,8 @@ enum {
   VTD_KNOB_SKINNY = 5,
   VTD_KNOB_F32_PP2 = 6,
   VTD_KNOB_STAGGER = 7,
-  VTD_KNOB_COUNT = 8
+  VTD_KNOB_GEMM_TR = 8,
+  VTD_KNOB_COUNT = 9
 };
 int vtd_set_knob(int knob, int value);
 int vtd_get_knob(int knob);

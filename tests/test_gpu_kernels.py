@@ -448,6 +448,58 @@ def test_gemm_variants_w4_pp2(L, cuda, monkeypatch, M, N, K, act, resid):
     assert torch.equal(outs["12"], outs["12s2"])     # the schedules differ in timing only
 
 
+@pytest.mark.parametrize("act,resid,fold,stat", [(0, False, True, False), (1, False, True, False),
+                                                 (0, True, False, True), (1, True, False, True),
+                                                 (2, False, False, False)])
+@pytest.mark.parametrize("tr", [0, 1])
+def test_gemm_accumulator_layouts(L, cuda, act, resid, fold, stat, tr):
+    """The 256-tile kernel's two accumulator layouts (knob VTD_KNOB_GEMM_TR: 0 = LDS-staged
+    row vectors, 1 = transposed accumulators, register-direct epilogue) on the forward's
+    epilogue combinations -- LayerNorm fold (row statistics from the wave's LDS table),
+    residual + partial statistics, activations -- against fp64."""
+    M, N, K = 12544, 768, 768
+    g = torch.Generator(device=cuda).manual_seed(7 + act + 2 * tr)
+    A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
+    Bt = (torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g, device=cuda)
+    x0 = torch.randn(M, N, generator=g, device=cuda).to(torch.bfloat16)
+    x = x0.clone()
+    e = L.VtdEpilogue()
+    e.bias, e.act, e.out, e.ldo, e.out_dtype = bias.data_ptr(), act, x.data_ptr(), N, 1
+    keep = []
+    if resid:
+        e.resid, e.ldr = x.data_ptr(), N
+    if fold:
+        mean = torch.randn(M, generator=g, device=cuda) * 0.1
+        rstd = torch.rand(M, generator=g, device=cuda) + 0.5
+        lnstat = torch.stack([mean, rstd], 1).contiguous()
+        colsum = Bt.float().sum(1).contiguous()
+        keep += [lnstat, colsum]
+        e.lnstat, e.colsum = lnstat.data_ptr(), colsum.data_ptr()
+    if stat:
+        st = torch.full((M, N // 64, 2), float("nan"), device=cuda)
+        keep.append(st)
+        e.statout, e.stat_ld = st.data_ptr(), N // 64
+    with L.knob(L.KNOB_GEMM_TR, tr):
+        L.check(L.lib.vtd_gemm(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, L.BF16,
+                               ctypes.byref(e), L.stream_ptr()), "vtd_gemm")
+    torch.cuda.synchronize()
+    acc = A.double() @ Bt.double().T
+    if fold:
+        acc = (acc - lnstat[:, :1].double() * colsum.double()[None, :]) * lnstat[:, 1:].double()
+    ref64 = _np_act(act, (acc + bias.double()).cpu().numpy())
+    if resid:
+        ref64 = ref64 + x0.double().cpu().numpy()
+    got = x.double().cpu().numpy()
+    err = np.abs(got - ref64) / np.maximum(np.abs(ref64), 1.0)
+    assert err.max() < 8e-3, (err.max(), np.argwhere(err >= 8e-3)[:5].tolist())
+    if stat:
+        blocks = x.float().view(M, N // 64, 64)
+        assert torch.allclose(st[..., 0], blocks.mean(-1), rtol=1e-5, atol=1e-5)
+        m2 = ((blocks - blocks.mean(-1, keepdim=True)) ** 2).sum(-1)
+        assert torch.allclose(st[..., 1], m2, rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.parametrize("variant", ["10", "12", "12s2"])
 def test_gemm_statout_variants(L, cuda, monkeypatch, variant):
     """The producer-side LayerNorm partial statistics on the 256-tile kernels (w4: the

@@ -43,6 +43,32 @@ STATOUT = {"attn_out_st", "mlp3_st"}
 LNFOLD = {"qkv_ln", "mlp1_ln"}
 
 
+def stamp_summary(call, M, N):
+    """Diagnostic library, VTD_PP2_DG=16: per-workgroup s_memtime stamps of one launch
+    (start, prologue landed, main loop done, epilogue issued; shader clocks) -> mean phase
+    lengths and, per XCC, the gap between a workgroup's end and the next start on the XCC."""
+    import numpy as np
+    fn = L.lib.vtd_diag_read_stamps
+    fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]
+    nwg = ((M + 255) // 256) * ((N + 255) // 256)
+    call()
+    torch.cuda.synchronize()
+    buf = np.zeros((nwg, 6), np.uint64)
+    assert fn(buf.ctypes.data, nwg) == 0
+    t = buf[:, :4].astype(np.int64)
+    pro, main, epi = t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], t[:, 3] - t[:, 2]
+    xcc = buf[:, 4].astype(np.int64)
+    spans = []
+    for x in np.unique(xcc):
+        tx = t[xcc == x]
+        spans.append(tx[:, 3].max() - tx[:, 0].min())
+    return {"stamp_cycles": {"prologue": int(np.median(pro)), "mainloop": int(np.median(main)),
+                             "epilogue": int(np.median(epi)),
+                             "tile": int(np.median(t[:, 3] - t[:, 0])),
+                             "xcc_span": int(np.median(spans)),
+                             "wg_per_xcc": int(nwg / max(1, len(spans)))}}
+
+
 def run(name, spec, reps, dev):
     M, N, K, act, od, res = spec
     g = torch.Generator(device=dev).manual_seed(0)
@@ -79,6 +105,8 @@ def run(name, spec, reps, dev):
     torch.cuda.synchronize()
     ms = t0.elapsed_time(t1) / reps
     res = {"shape": name, "us": round(ms * 1e3, 1), "tflops": round(2 * M * N * K / ms / 1e9, 1)}
+    if os.environ.get("VTD_PP2_DG") == "16":
+        res.update(stamp_summary(call, M, N))
     if os.environ.get("VTD_GEMM_SPLIT2"):
         # the same problem as two M-halves on two streams at once (the forward's two-stream
         # micro-batching), and the two halves back to back on one stream

@@ -23,11 +23,16 @@ def tiles(M, N):
 
 
 def shape_of(kernel, grid):
+    """gemm_bench shape of a pp2 launch: tile count + the epilogue code's residual and
+    activation bits (kernel template argument)."""
+    import re
     wg = grid // 512 if grid % 512 == 0 else grid
-    resid = "<76" in kernel or "<77" in kernel or "<12" in kernel or "<13" in kernel or "<14" in kernel
-    for name, (M, N, K, act, od, res) in SHAPES.items():
-        if (tiles(M, N) == wg and res == resid and not name.endswith("_noact") and
-                not name.endswith(("_st", "_ln"))):
+    m = re.search(r"pp2_kernel<(-?\d+)", kernel)
+    code = int(m.group(1)) if m else -1
+    resid, act = code >= 0 and bool(code & 8), code & 3 if code >= 0 else -1
+    for name, (M, N, K, a, od, res) in SHAPES.items():
+        if (tiles(M, N) == wg and res == resid and (a != 0) == (act != 0) and
+                not name.endswith(("_noact", "_st", "_ln", "_h"))):
             return name
     return f"{kernel[:40]}|{wg}"
 

@@ -212,7 +212,8 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(int M, int N, int K,
 
 constexpr int BBM = 256, BBN = 256, BNT = 512;
 constexpr int BSTAGE = (BBM + BBN) * KB;     // 64 KiB per stage
-static_assert(8 * 32 * 68 * 4 <= 2 * BSTAGE, "epilogue staging must fit the stages");
+static_assert(8 * 32 * 68 * 4 + 8 * 128 * 8 <= 2 * BSTAGE,
+              "epilogue staging + LayerNorm-fold row tables must fit the stages");
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) const void gbl_void_t;
@@ -232,6 +233,7 @@ typedef __attribute__((address_space(1))) const void gbl_void_t;
 // residual reads and output writes are 16-B per lane (one 128-B line per 8 lanes).
 // DG (diagnostic build only, wrong outputs): 1 = no partial statistics, 2 = no residual
 // loads, 4 = no output stores (values kept live), 8 = no epilogue at all
+// lst (EPI_LNF): the wave's LayerNorm-fold row statistics in LDS, local rows 0..127
 template <int EPI, int PR = 32, int DG = 0>
 __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* ep, int lane,
                                               int m_base, int n_base, const EpiArgs& e,
@@ -296,7 +298,7 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
       const int row = it * 8 + rsub;
       f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + row * ES + c8);
       f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + row * ES + c8 + 4);
-      if constexpr (LNF) epi_lnfold8(e, lst, m_base + p * PR + row, p * PR + row, cs0, cs1, v0, v1);
+      if constexpr (LNF) epi_lnfold8_st(lst[p * PR + row], cs0, cs1, v0, v1);
       v0 += b0;
       v1 += b1;
       if constexpr ((EPI & EPI_RA) != 0) epi_rowadd8(e, m_base + p * PR + row, n_base + c8, v0, v1);
@@ -344,8 +346,10 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
         else store_out16(static_cast<bf16_t*>(e.out) + idx, o);
         if constexpr (STAT) {      // the row's 64 columns live in 8 consecutive lanes
           // block mean, then the centred sum of squares (DPP sums, no LDS traffic)
-          const float mean = sum8_dpp(bf16x8_sum(o)) * (1.f / 64.f);
-          const float m2 = sum8_dpp(bf16x8_m2(o, mean));
+          f32x2 pv[4];
+          bf16x8_unpack(o, pv);
+          const float mean = sum8_dpp(pairs_sum(pv)) * (1.f / 64.f);
+          const float m2 = sum8_dpp(pairs_m2(pv, mean));
           if ((lane & 7) == 7)
             e.statout[(int64_t)(m_base + p * PR + row) * e.stat_ld + (n_base >> 6)] =
                 float2{mean, m2};
@@ -573,7 +577,8 @@ __device__ __forceinline__ void pp2_issue(char* smem, const PP2BufSrc& src, int 
 
 template <bool TR, bool F32 = false>
 __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, const PP2BufSrc& src,
-                                             int nk, int wave, int wm, int wn, int fr, int fg) {
+                                             int nk, int wave, int wm, int wn, int fr, int fg,
+                                             uint64_t* t_prologue = nullptr) {
   // prologue: tile 0 complete, tile 1's X0/Y0/Y1 in flight
   pp2_issue<0>(smem, src, wave, 0, 0);
   pp2_issue<2>(smem, src, wave, 0, 0);
@@ -588,6 +593,7 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   pp_barrier();
+  if (t_prologue) *t_prologue = __builtin_amdgcn_s_memtime();   // diagnostic stamps only
   if (wm == 1) pp_barrier();                 // stagger G1 by one barrier
   const int ra = wm * 64, rb = wn * 32;      // group rows of this wave's quads
   bf16x8 a[4][2], b0[2][2], b1[2][2];
@@ -682,6 +688,11 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
 #pragma unroll
   for (int i0 = 0; i0 < 8; i0 += 4) {
     f32x4 rv[4][2][2];
+    float2 st[4];                      // LayerNorm fold: the (mean, rstd) of rows 16 (i0 + i) + fr
+    if constexpr (LNF) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) st[i] = lst[16 * (i0 + i) + fr];
+    }
     if constexpr (RPRE) {
       if (i0 == 0) load_raw(4, rraw[1]);
     } else if constexpr (RESID) {
@@ -703,7 +714,7 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
         f32x4 v1 = acc[i0 + i][2 * jp + 1];
         const int mrow = m_base + 16 * (i0 + i) + fr, ncol = n_base + 32 * jp + 8 * fg;
         if constexpr (LNF)
-          epi_lnfold8(e, lst, mrow, 16 * (i0 + i) + fr, cs[jp][0], cs[jp][1], v0, v1);
+          epi_lnfold8_st(st[i], cs[jp][0], cs[jp][1], v0, v1);
         v0 += bias[jp][0];
         v1 += bias[jp][1];
         if constexpr ((EPI & EPI_RA) != 0) epi_rowadd8(e, mrow, ncol, v0, v1);
@@ -768,6 +779,11 @@ __device__ __forceinline__ void epilogue_direct_generic(const f32x4 (&acc)[8][4]
   }
 }
 
+#if VTD_DIAG
+constexpr int kStampSlots = 16384;
+__device__ uint64_t g_pp2_stamps[kStampSlots * 6];
+#endif
+
 // ksplit > 1 (split-K, EPI_PARTIAL or EPI_GENERIC without bias / activation): the grid holds
 // ksplit x tiles workgroups; workgroup v (after the XCD remap) takes split v / tiles of tile
 // v % tiles (neighbours on an XCD share a K range, so their panels are the same lines) and
@@ -808,8 +824,38 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fg = lane >> 4;
-  pp2_mainloop<TR>(acc, smem, src, nk, wave, wm, wn, fr, fg);
+  uint64_t ts[4] = {0, 0, 0, 0};
+  if constexpr ((DG & 16) != 0) ts[0] = __builtin_amdgcn_s_memtime();
+  pp2_mainloop<TR>(acc, smem, src, nk, wave, wm, wn, fr, fg, (DG & 16) ? &ts[1] : nullptr);
+  if constexpr ((DG & 16) != 0) ts[2] = __builtin_amdgcn_s_memtime();
   const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
+#if VTD_DIAG
+  // DG & 16 (diagnostic build): per-workgroup s_memtime stamps of wave 0 -- start, prologue
+  // landed, main loop done, epilogue stores issued -- and the XCC id, at g_pp2_stamps[bid]
+  auto stamp = [&]() {
+    if constexpr ((DG & 16) != 0) {
+      ts[3] = __builtin_amdgcn_s_memtime();
+      if (wave == 0 && lane == 0 && bid < kStampSlots) {
+        g_pp2_stamps[bid * 6 + 0] = ts[0];
+        g_pp2_stamps[bid * 6 + 1] = ts[1];
+        g_pp2_stamps[bid * 6 + 2] = ts[2];
+        g_pp2_stamps[bid * 6 + 3] = ts[3];
+        g_pp2_stamps[bid * 6 + 4] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
+        g_pp2_stamps[bid * 6 + 5] = (uint64_t)tile;
+      }
+    }
+  };
+#else
+  auto stamp = [&]() {};
+#endif
+  // LayerNorm fold: the wave's 128 row statistics into a wave-private LDS table past the
+  // epilogue staging regions (stages are free after the main loop's last barrier); the
+  // epilogues read a row's pair from it (a broadcast ds_read_b64, no lane shuffles)
+  float2* const lds_st = reinterpret_cast<float2*>(smem + 8 * 32 * 68 * 4) + wave * 128;
+  if constexpr (EPI != EPI_GENERIC && (EPI & EPI_LNF) != 0) {
+    lds_st[lane] = lst[0];
+    lds_st[64 + lane] = lst[1];
+  }
   if constexpr ((DG & 8) != 0) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -820,7 +866,8 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
   if constexpr (TR) {
     if constexpr (EPI != EPI_GENERIC) {
       if (m0 + BBM <= M && n0 + BBN <= N) {
-        epilogue_direct<EPI, DG>(acc, lane, m_base, n_base, e, lst);
+        epilogue_direct<EPI, DG>(acc, lane, m_base, n_base, e, lds_st);
+        stamp();
         return;
       }
     }
@@ -831,7 +878,8 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
   float* ep = reinterpret_cast<float*>(smem) + wave * 32 * 68;
   if constexpr (EPI != EPI_GENERIC) {
     if (m0 + BBM <= M && n0 + BBN <= N) {
-      epilogue_fast<EPI, 32, DG>(acc, ep, lane, m_base, n_base, e, lst);
+      epilogue_fast<EPI, 32, DG>(acc, ep, lane, m_base, n_base, e, lds_st);
+      stamp();
       return;
     }
   }
@@ -1342,8 +1390,10 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
     e.ngw = ngw;
     const int code = pp2_code(epi);
     // transposed accumulators + register-direct epilogue for activation layers (mlp1 -5 %,
-    // mlp2 -1.5 %), LDS-staged row vectors for the others (attn_out -10 %, mlp3 -4 %)
-    const bool tr = e.act != VTD_ACT_NONE;
+    // mlp2 -1.5 %), LDS-staged row vectors for the others (attn_out -10 %, mlp3 -4 %);
+    // knob VTD_KNOB_GEMM_TR: 0 = never, 1 = always
+    const int ktr = knob(VTD_KNOB_GEMM_TR);
+    const bool tr = ktr >= 0 ? ktr != 0 : e.act != VTD_ACT_NONE;
     const dim3 g(tiles_m * tiles_n);
 #if VTD_DIAG
     // epilogue ablation (wrong outputs): VTD_PP2_DG = the DG bits of epilogue_fast /
@@ -1362,7 +1412,9 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
                                 reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, false, 4>),
                                 reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, true, 4>),
                                 reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, false, 8>),
-                                reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, true, 8>)})
+                                reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, true, 8>),
+                                reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, false, 16>),
+                                reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, true, 16>)})
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
         });
 #define VTD_DG_L(D)                                                                                \
@@ -1372,7 +1424,7 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
     else hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, false, D>), g, dim3(BNT), 2 * BSTAGE,      \
                             stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e, 1);          \
   }
-        VTD_DG_L(1) VTD_DG_L(2) VTD_DG_L(4) VTD_DG_L(8)
+        VTD_DG_L(1) VTD_DG_L(2) VTD_DG_L(4) VTD_DG_L(8) VTD_DG_L(16)
 #undef VTD_DG_L
       };
       switch (code) {
@@ -1603,4 +1655,10 @@ extern "C" int vtd_gemm_splitk_choice(int M, int N, int K, int dtype) {
 #if VTD_DIAG
 // present in the diagnostic build only (tests select the w4 / x4 comparisons by it)
 extern "C" int vtd_diag_build(void) { return 1; }
+// the pp2 kernel's per-workgroup stamps (VTD_PP2_DG=16): n slots of 6 uint64 each
+extern "C" int vtd_diag_read_stamps(uint64_t* host, int n) {
+  n = std::min(n, vtd::kStampSlots);
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(vtd::g_pp2_stamps), (size_t)n * 6 * 8, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
+}
 #endif

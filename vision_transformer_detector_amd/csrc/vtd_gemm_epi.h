@@ -88,24 +88,36 @@ __device__ __forceinline__ float xsum32(float v) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// sum of the 8 bf16 values packed in o
-__device__ __forceinline__ float bf16x8_sum(const i32x4& o) {
-  float s = 0.f;
+// the 8 bf16 values packed in o as four f32 pairs (element order lo, hi of each word)
+__device__ __forceinline__ void bf16x8_unpack(const i32x4& o, f32x2 (&p)[4]) {
 #pragma unroll
   for (int w = 0; w < 4; ++w)
-    s += __uint_as_float((uint32_t)o[w] << 16) + __uint_as_float((uint32_t)o[w] & 0xffff0000u);
-  return s;
+    p[w] = f32x2{__uint_as_float((uint32_t)o[w] << 16),
+                 __uint_as_float((uint32_t)o[w] & 0xffff0000u)};
+}
+// sum of 8 unpacked values (pairwise tree through the packed VALU)
+__device__ __forceinline__ float pairs_sum(const f32x2 (&p)[4]) {
+  const f32x2 t = (p[0] + p[1]) + (p[2] + p[3]);
+  return t.x + t.y;
+}
+// sum of squared deviations from `mean` of 8 unpacked values
+__device__ __forceinline__ float pairs_m2(const f32x2 (&p)[4], float mean) {
+  const f32x2 m = {mean, mean};
+  const f32x2 d0 = p[0] - m, d1 = p[1] - m, d2 = p[2] - m, d3 = p[3] - m;
+  const f32x2 q = (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+  return q.x + q.y;
+}
+// sum of the 8 bf16 values packed in o
+__device__ __forceinline__ float bf16x8_sum(const i32x4& o) {
+  f32x2 p[4];
+  bf16x8_unpack(o, p);
+  return pairs_sum(p);
 }
 // sum of squared deviations from `mean` of the 8 bf16 values packed in o
 __device__ __forceinline__ float bf16x8_m2(const i32x4& o, float mean) {
-  float q = 0.f;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    const float lo = __uint_as_float((uint32_t)o[w] << 16) - mean;
-    const float hi = __uint_as_float((uint32_t)o[w] & 0xffff0000u) - mean;
-    q += lo * lo + hi * hi;
-  }
-  return q;
+  f32x2 p[4];
+  bf16x8_unpack(o, p);
+  return pairs_m2(p, mean);
 }
 // total over the 8 consecutive lanes of a half-row, in all 8 lanes: DPP quad xor 1,
 // quad xor 2, then row_half_mirror (lane i <-> 7 - i: the other quad)
@@ -270,9 +282,16 @@ __device__ __forceinline__ void epi_out2_8(const EpiArgs& e, int m, int n, f32x4
   *reinterpret_cast<i32x4*>(static_cast<bf16_t*>(e.out2) + (int64_t)m * e.ldo2 + n) = o;
 }
 
-// LayerNorm fold of 8 contiguous columns of row m (c0, c1 = colsum of those columns).
-// lst (the pp2 kernels): the (mean, rstd) of the wave's 128 rows, loaded before the K
-// loop, lane l holding local rows l (lst[0]) and 64 + l (lst[1]); lr = m's local row.
+// LayerNorm fold of 8 contiguous columns with the row's (mean, rstd) st (c0, c1 = colsum of
+// those columns).
+__device__ __forceinline__ void epi_lnfold8_st(float2 st, f32x4 c0, f32x4 c1, f32x4& v0,
+                                               f32x4& v1) {
+  v0 = (v0 - st.x * c0) * st.y;
+  v1 = (v1 - st.x * c1) * st.y;
+}
+// The same with the row's statistics fetched by lane shuffles (the w4 kernel): lst = the
+// (mean, rstd) of the wave's 128 rows, lane l holding local rows l (lst[0]) and 64 + l
+// (lst[1]); lr = m's local row.
 __device__ __forceinline__ void epi_lnfold8(const EpiArgs& e, const float2* lst, int m, int lr,
                                             f32x4 c0, f32x4 c1, f32x4& v0, f32x4& v1) {
   float2 st;
