@@ -386,7 +386,12 @@ int vtd_profile_read(double* ms, int64_t* launches, double* flops, int n_classes
  *   VTD_KNOB_STAGGER (VTD_STAGGER): the two-stream split's second micro-batch starts k stages
  *     (patch embedding, encoder layers) behind the first (default 0: in phase).
  *   VTD_KNOB_GEMM_TR (VTD_GEMM_TR): 256-tile bf16 GEMM accumulator layout, 1 = transposed
- *     (register-direct epilogue) for every layer, 0 = for none (default: activation layers). */
+ *     (register-direct epilogue) for every layer, 0 = for none (default: activation layers).
+ *   VTD_KNOB_FIN_WGS (VTD_FIN_WGS): LayerNorm-statistics finalize as n grid-stride
+ *     workgroups of 1024 threads (default: one 256-thread workgroup per 256 rows).
+ *   VTD_KNOB_GEMM_TPW (VTD_GEMM_TPW): consecutive 256 x 256 output tiles per bf16 GEMM
+ *     workgroup (default 1); with more, the next tile's first K-stage loads during the
+ *     current tile's epilogue. */
 enum {
   VTD_KNOB_ATTN_VARIANT = 0,
   VTD_KNOB_ATTN_GRID = 1,
@@ -397,7 +402,9 @@ enum {
   VTD_KNOB_F32_PP2 = 6,
   VTD_KNOB_STAGGER = 7,
   VTD_KNOB_GEMM_TR = 8,
-  VTD_KNOB_COUNT = 9
+  VTD_KNOB_FIN_WGS = 9,
+  VTD_KNOB_GEMM_TPW = 10,
+  VTD_KNOB_COUNT = 11
 };
 int vtd_set_knob(int knob, int value);
 int vtd_get_knob(int knob);

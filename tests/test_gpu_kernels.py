@@ -721,7 +721,13 @@ def test_gemm_statout_and_finalize(L, cuda, N, K, act, resid, offset):
     st = torch.zeros(M, 2, device=cuda)
     L.check(L.lib.vtd_layernorm_stats_finalize(part.data_ptr(), M, slots, N, 1e-3, st.data_ptr(),
                                                L.stream_ptr()), "finalize")
+    # the grid-stride form (knob VTD_KNOB_FIN_WGS, few 1024-thread workgroups): same bits
+    st2 = torch.full((M, 2), float("nan"), device=cuda)
+    with L.knob(L.KNOB_FIN_WGS, 3):
+        L.check(L.lib.vtd_layernorm_stats_finalize(part.data_ptr(), M, slots, N, 1e-3,
+                                                   st2.data_ptr(), L.stream_ptr()), "finalize")
     torch.cuda.synchronize()
+    assert torch.equal(st, st2)
     xs = x.double().cpu().numpy().reshape(M, slots, 64)
     got = part.double().cpu().numpy()
     bm = xs.mean(2)
@@ -845,3 +851,59 @@ def test_gemm_statout_needs_a_specialised_epilogue(L, cuda):
     assert torch.isfinite(stat).all()
     blocks = x.float().view(M, N // 64, 64)
     assert torch.allclose(stat[..., 0], blocks.mean(-1), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("M,N,K,act,mode", [
+    (4100, 2100, 192, 1, "bf16"),         # ragged M / N: generic epilogue on edge tiles
+    (8192, 1024, 64, 1, "bf16"),          # one K-step: the prefetched stage is the whole loop
+    (12544, 768, 768, 0, "stat"),         # residual + partial statistics (attention_output)
+    (12544, 768, 768, 1, "fold"),         # LayerNorm fold + gelu (mlp1)
+    (12544, 2304, 768, 0, "fold"),        # LayerNorm fold (query/key/value)
+    (6000, 1544, 3072, 1, "bf16")])       # (all >= 128 tiles: the pp2 kernels)
+@pytest.mark.parametrize("tpw", [2, 3, 5])
+def test_gemm_tiles_per_workgroup(L, cuda, M, N, K, act, mode, tpw):
+    """Several output tiles per pp2 workgroup (knob VTD_KNOB_GEMM_TPW, gemm_tn_bf16_pp2_mt_kernel
+    for the forward's epilogue codes; the next tile's first K-stage is loaded during the
+    current tile's epilogue): every tile is computed by the same instructions, so the outputs
+    (and statistics) equal the one-tile launch bit for bit -- tile counts not divisible by
+    tpw, ragged edges and one-K-step loops included."""
+    g = torch.Generator(device=cuda).manual_seed(M + K + act)
+    A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
+    Bt = (torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g, device=cuda)
+    f32 = mode == "f32resid"
+    r0 = torch.randn(M, N, generator=g, device=cuda)
+    if not f32:
+        r0 = r0.to(torch.bfloat16)
+    keep = []
+
+    def run():
+        x = r0.clone()
+        e = L.VtdEpilogue()
+        e.bias, e.act, e.out, e.ldo, e.out_dtype = bias.data_ptr(), act, x.data_ptr(), N, 0 if f32 else 1
+        st = None
+        if mode in ("f32resid", "stat"):
+            e.resid, e.ldr = x.data_ptr(), N
+        if mode == "stat":
+            st = torch.full((M, N // 64, 2), float("nan"), device=cuda)
+            e.statout, e.stat_ld = st.data_ptr(), N // 64
+        if mode == "fold":
+            gg = torch.Generator(device=cuda).manual_seed(3)
+            lnstat = torch.stack([torch.randn(M, generator=gg, device=cuda) * 0.1,
+                                  torch.rand(M, generator=gg, device=cuda) + 0.5], 1).contiguous()
+            colsum = Bt.float().sum(1).contiguous()
+            keep.extend([lnstat, colsum])
+            e.lnstat, e.colsum = lnstat.data_ptr(), colsum.data_ptr()
+        L.check(L.lib.vtd_gemm(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, L.BF16,
+                               ctypes.byref(e), L.stream_ptr()), "vtd_gemm")
+        torch.cuda.synchronize()
+        return x, st
+
+    with L.knob(L.KNOB_GEMM_TPW, 1):
+        x1, s1 = run()
+    with L.knob(L.KNOB_GEMM_TPW, tpw):
+        x2, s2 = run()
+    assert not torch.isnan(x1.float()).any()
+    assert torch.equal(x1, x2)
+    if s1 is not None:
+        assert torch.equal(s1, s2)

@@ -53,13 +53,14 @@ def test_removed_switches_are_not_read_by_the_library(L):
     assert not hasattr(L.lib, "vtd_diag_build")
     # the run-time knobs are read from the environment once per process (vtd_set_knob)
     for name in (b"VTD_ATTN_VARIANT", b"VTD_ATTN_GRID", b"VTD_GEMM_NGW", b"VTD_SPLITK",
-                 b"VTD_JPEG_CHUNK_BITS", b"VTD_SKINNY", b"VTD_F32_PP2", b"VTD_STAGGER", b"VTD_GEMM_TR"):
+                 b"VTD_JPEG_CHUNK_BITS", b"VTD_SKINNY", b"VTD_F32_PP2", b"VTD_STAGGER", b"VTD_GEMM_TR",
+                 b"VTD_FIN_WGS", b"VTD_GEMM_TPW"):
         assert name + b"\0" in blob, name
 
 
 def test_knobs_set_get_and_restore(L):
     """vtd_set_knob returns the previous value; out-of-range knobs are rejected."""
-    for k in range(L.KNOB_GEMM_TR + 1):
+    for k in range(L.KNOB_GEMM_TPW + 1):
         prev = L.lib.vtd_get_knob(k)
         assert L.lib.vtd_set_knob(k, 7) == prev
         assert L.lib.vtd_get_knob(k) == 7

@@ -57,16 +57,27 @@ def stamp_summary(call, M, N):
     assert fn(buf.ctypes.data, nwg) == 0
     t = buf[:, :4].astype(np.int64)
     pro, main, epi = t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], t[:, 3] - t[:, 2]
-    xcc = buf[:, 4].astype(np.int64)
-    spans = []
-    for x in np.unique(xcc):
-        tx = t[xcc == x]
-        spans.append(tx[:, 3].max() - tx[:, 0].min())
+    r0, r1 = buf[:, 4].astype(np.int64), buf[:, 5].astype(np.int64)   # 100 MHz real time
+    clk_ghz = float(np.median((t[:, 3] - t[:, 0]) / np.maximum(r1 - r0, 1))) / 10.0
+    span_us = (r1.max() - r0.min()) / 100.0
+    busy_us = (r1 - r0).sum() / 100.0
+    # running workgroups over time: the mean over the launch span, the share of the span with
+    # >= 240 of the 256 CUs busy
+    ev = np.concatenate([np.stack([r0, np.ones_like(r0)], 1), np.stack([r1, -np.ones_like(r1)], 1)])
+    ev = ev[np.lexsort((ev[:, 1], ev[:, 0]))]
+    run, full, last = 0, 0, ev[0, 0]
+    for tt, d in ev:
+        if run >= 240:
+            full += tt - last
+        run += d
+        last = tt
     return {"stamp_cycles": {"prologue": int(np.median(pro)), "mainloop": int(np.median(main)),
                              "epilogue": int(np.median(epi)),
-                             "tile": int(np.median(t[:, 3] - t[:, 0])),
-                             "xcc_span": int(np.median(spans)),
-                             "wg_per_xcc": int(nwg / max(1, len(spans)))}}
+                             "tile": int(np.median(t[:, 3] - t[:, 0]))},
+            "clock_ghz": round(clk_ghz, 3), "span_us": round(span_us, 1),
+            "mean_running_wg": round(busy_us / max(span_us, 1e-9), 1),
+            "full_share": round(full / 100.0 / max(span_us, 1e-9), 3),
+            "tile_us": round(float(np.median(r1 - r0)) / 100.0, 2)}
 
 
 def run(name, spec, reps, dev):

@@ -27,7 +27,8 @@ MAP_CLASSES, MAP_LATEST, MAP_PER_IMAGE, MAP_MAX_BOXES = 80, 3, 14, 64
 F32, BF16, FP8 = 0, 1, 2
 # run-time A/B knobs (vtd_set_knob; -1 = the library default)
 KNOB_ATTN_VARIANT, KNOB_ATTN_GRID, KNOB_GEMM_NGW, KNOB_SPLITK, KNOB_JPEG_CHUNK_BITS = 0, 1, 2, 3, 4
-KNOB_SKINNY, KNOB_F32_PP2, KNOB_STAGGER, KNOB_GEMM_TR = 5, 6, 7, 8
+KNOB_SKINNY, KNOB_F32_PP2, KNOB_STAGGER, KNOB_GEMM_TR, KNOB_FIN_WGS = 5, 6, 7, 8, 9
+KNOB_GEMM_TPW = 10
 ACT_NONE, ACT_GELU_TANH, ACT_MISH = 0, 1, 2
 STATUS = {0: "VTD_OK", -1: "VTD_ERR_INVALID_ARG", -2: "VTD_ERR_UNSUPPORTED",
           -3: "VTD_ERR_HIP", -4: "VTD_ERR_WORKSPACE"}

@@ -514,19 +514,23 @@ __global__ __launch_bounds__(256) void ln_stats_finalize_kernel(const float2* __
 // The same with the slot count known at compile time: the row's S partials are loaded as
 // S / 2 16-B words before any arithmetic (one memory round trip instead of a dependent
 // chain); same operations in the same order as ln_stats_finalize_kernel (identical results).
+// Grid-stride over the rows (gridDim.x * blockDim.x threads): launched with few large
+// workgroups in the two-stream forward, where every workgroup waits for a CU the other
+// stream's GEMM tile vacates (knob VTD_KNOB_FIN_WGS).
 template <int S>
-__global__ __launch_bounds__(256) void ln_stats_finalize_s_kernel(const float4* __restrict__ part,
-                                                                  int64_t rows, int D, float eps,
-                                                                  float2* __restrict__ stat) {
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (r >= rows) return;
-  f32x4 v[S / 2];
+__global__ __launch_bounds__(1024) void ln_stats_finalize_s_kernel(const float4* __restrict__ part,
+                                                                   int64_t rows, int D, float eps,
+                                                                   float2* __restrict__ stat) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    f32x4 v[S / 2];
 #pragma unroll
-  for (int b = 0; b < S / 2; ++b) {
-    const float4 w = part[r * (S / 2) + b];
-    v[b] = f32x4{w.x, w.y, w.z, w.w};
+    for (int b = 0; b < S / 2; ++b) {
+      const float4 w = part[r * (S / 2) + b];
+      v[b] = f32x4{w.x, w.y, w.z, w.w};
+    }
+    stat[r] = ln_merge_partials<S>(v, D, eps);
   }
-  stat[r] = ln_merge_partials<S>(v, D, eps);
 }
 
 // LayerNorm fold of one consumer Dense layer (one-time weight preparation): one wave per
@@ -779,9 +783,17 @@ int ln_stats_finalize_launch(const float* part, int64_t rows, int slots, int D, 
   if (slots == 12 || slots == 16) {
     if (reinterpret_cast<uintptr_t>(part) % 16 == 0) {
       auto k = slots == 12 ? ln_stats_finalize_s_kernel<12> : ln_stats_finalize_s_kernel<16>;
-      hipLaunchKernelGGL(k, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st,
-                         reinterpret_cast<const float4*>(part), rows, D, eps,
-                         reinterpret_cast<float2*>(stat));
+      // knob VTD_KNOB_FIN_WGS = n > 0: n workgroups of 1024 threads (grid-stride)
+      const int fw = knob(VTD_KNOB_FIN_WGS);
+      const int64_t need = (rows + 1023) / 1024;
+      if (fw > 0)
+        hipLaunchKernelGGL(k, dim3((unsigned)std::min<int64_t>(fw, need)), dim3(1024), 0, st,
+                           reinterpret_cast<const float4*>(part), rows, D, eps,
+                           reinterpret_cast<float2*>(stat));
+      else
+        hipLaunchKernelGGL(k, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st,
+                           reinterpret_cast<const float4*>(part), rows, D, eps,
+                           reinterpret_cast<float2*>(stat));
       VTD_LAUNCH_CHECK("layernorm_stats_finalize");
       return VTD_OK;
     }

@@ -234,10 +234,31 @@ typedef __attribute__((address_space(1))) const void gbl_void_t;
 // DG (diagnostic build only, wrong outputs): 1 = no partial statistics, 2 = no residual
 // loads, 4 = no output stores (values kept live), 8 = no epilogue at all
 // lst (EPI_LNF): the wave's LayerNorm-fold row statistics in LDS, local rows 0..127
-template <int EPI, int PR = 32, int DG = 0>
+// pf (multi-tile workgroups): issues the next tile's first K-stage DMA.  Called once the
+// epilogue's own operand loads are in flight (bias, then the residual rows of the first two
+// passes), so that no wait on those loads also waits for the DMA (vmcnt retires in order).
+struct NoPF {
+  __device__ void operator()() const {}
+};
+
+// Four (mean, rstd) rows of the wave's LayerNorm-fold table at byte offsets addr + O0..O3
+// (LDS address = the low 32 bits of the generic pointer).  Inline asm with its own wait:
+// reads the compiler schedules itself get a vmcnt(0) after the next tile's LDS-bound DMA
+// (pf), which would serialise the epilogue behind that prefetch.
+template <int O0, int O1, int O2, int O3>
+__device__ __forceinline__ void lds_read4_b64(const void* p, float2 (&o)[4]) {
+  const uint32_t a = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p));
+  asm volatile(
+      "ds_read_b64 %0, %4 offset:%5\n\tds_read_b64 %1, %4 offset:%6\n\t"
+      "ds_read_b64 %2, %4 offset:%7\n\tds_read_b64 %3, %4 offset:%8\n\ts_waitcnt lgkmcnt(0)"
+      : "=v"(o[0]), "=v"(o[1]), "=v"(o[2]), "=v"(o[3])
+      : "v"(a), "i"(O0), "i"(O1), "i"(O2), "i"(O3)
+      : "memory");
+}
+template <int EPI, int PR = 32, int DG = 0, typename PF = NoPF>
 __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* ep, int lane,
                                               int m_base, int n_base, const EpiArgs& e,
-                                              const float2* lst = nullptr) {
+                                              const float2* lst = nullptr, PF pf = PF{}) {
   constexpr int ACT = EPI & 3;
   constexpr bool OUT_BF16 = (EPI & 4) != 0;
   constexpr bool RESID = (EPI & 8) != 0 && !(DG & 2);
@@ -273,6 +294,7 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
     }
   };
   if constexpr (RPRE) load_raw(0, rraw[0]);
+  else pf();
 #pragma unroll
   for (int p = 0; p < 128 / PR; ++p) {
 #pragma unroll
@@ -284,6 +306,18 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
           ep[(i * 16 + fg * 4 + r2) * ES + j * 16 + fr] = acc[p * NB + i][j][r2];
     if constexpr (RPRE) {
       if (p + 1 < 128 / PR) load_raw(p + 1, rraw[(p + 1) & 1]);
+      if (p == 0) pf();
+    }
+    // LayerNorm fold, with a prefetch (pf): rows p * PR + it * 8 + rsub read up front by
+    // lds_read4_b64 (without one, each row's pair is read where it is used)
+    constexpr bool ASM_ST = LNF && !std::is_same<PF, NoPF>::value;
+    float2 stv[4];
+    if constexpr (ASM_ST) {
+      static_assert(PR == 32, "the fold's table reads assume 32-row passes");
+      if (p == 0) lds_read4_b64<0, 64, 128, 192>(lst + rsub, stv);
+      else if (p == 1) lds_read4_b64<256, 320, 384, 448>(lst + rsub, stv);
+      else if (p == 2) lds_read4_b64<512, 576, 640, 704>(lst + rsub, stv);
+      else lds_read4_b64<768, 832, 896, 960>(lst + rsub, stv);
     }
     f32x4 rv[NIT][2];
     if constexpr (RESID && !RPRE) {
@@ -298,7 +332,8 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
       const int row = it * 8 + rsub;
       f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + row * ES + c8);
       f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + row * ES + c8 + 4);
-      if constexpr (LNF) epi_lnfold8_st(lst[p * PR + row], cs0, cs1, v0, v1);
+      if constexpr (ASM_ST) epi_lnfold8_st(stv[it], cs0, cs1, v0, v1);
+      else if constexpr (LNF) epi_lnfold8_st(lst[p * PR + row], cs0, cs1, v0, v1);
       v0 += b0;
       v1 += b1;
       if constexpr ((EPI & EPI_RA) != 0) epi_rowadd8(e, m_base + p * PR + row, n_base + c8, v0, v1);
@@ -540,17 +575,20 @@ struct PP2BufSrc {
 template <bool TR, typename T = bf16_t>
 __device__ __forceinline__ void pp2b_sources(PP2BufSrc& s, const T* A, int lda, int M,
                                              const T* Bt, int ldb, int N, int m0, int n0,
-                                             int wave, int lane, int k0 = 0) {
+                                             int wave, int lane, int k0 = 0, bool valid = true) {
   // records = bytes from the tile base to the end of the operand (clamped to 32 bits); all
   // offsets are in range because rows are clamped to the last valid row.  k0: first K
   // element of the loop (split-K ranges), folded into the base.
   constexpr int ES = (int)sizeof(T);
   const int64_t ra_bytes = (int64_t)(M - m0) * lda * ES - ES * k0,
                 rb_bytes = (int64_t)(N - n0) * ldb * ES - ES * k0;
+  // !valid: zero records -- every load out of range (no memory traffic)
   s.ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(A + (int64_t)m0 * lda + k0), 0,
-                                           (int)std::min<int64_t>(ra_bytes, 0x7fffffff), 0x00020000);
+                                           valid ? (int)std::min<int64_t>(ra_bytes, 0x7fffffff) : 0,
+                                           0x00020000);
   s.rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(Bt + (int64_t)n0 * ldb + k0), 0,
-                                           (int)std::min<int64_t>(rb_bytes, 0x7fffffff), 0x00020000);
+                                           valid ? (int)std::min<int64_t>(rb_bytes, 0x7fffffff) : 0,
+                                           0x00020000);
   const int prow = lane >> 3, pchunk = (lane & 7) ^ prow;
 #pragma unroll
   for (int g = 0; g < 4; ++g)
@@ -575,15 +613,22 @@ __device__ __forceinline__ void pp2_issue(char* smem, const PP2BufSrc& src, int 
                                              kt * 128, 0, 0);
 }
 
+// pre: K-tile 0 was issued by the caller (pp2_prefetch, during the previous output tile's
+// epilogue, whose LDS staging lies past stage 0): wait until every wave has left that epilogue
+// before K-tile 1 is loaded over it.
 template <bool TR, bool F32 = false>
 __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, const PP2BufSrc& src,
                                              int nk, int wave, int wm, int wn, int fr, int fg,
-                                             uint64_t* t_prologue = nullptr) {
+                                             uint64_t* t_prologue = nullptr, bool pre = false) {
   // prologue: tile 0 complete, tile 1's X0/Y0/Y1 in flight
-  pp2_issue<0>(smem, src, wave, 0, 0);
-  pp2_issue<2>(smem, src, wave, 0, 0);
-  pp2_issue<3>(smem, src, wave, 0, 0);
-  pp2_issue<1>(smem, src, wave, 0, 0);
+  if (!pre) {
+    pp2_issue<0>(smem, src, wave, 0, 0);
+    pp2_issue<2>(smem, src, wave, 0, 0);
+    pp2_issue<3>(smem, src, wave, 0, 0);
+    pp2_issue<1>(smem, src, wave, 0, 0);
+  } else {
+    pp_barrier();
+  }
   if (nk > 1) {
     pp2_issue<0>(smem, src, wave, 1, 1);
     pp2_issue<2>(smem, src, wave, 1, 1);
@@ -653,10 +698,10 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
 // for accumulator row block i and column half jp, output row m_base + 16 i + fr and the 8
 // contiguous columns n_base + 32 jp + 8 fg + 0..7 (acc[i][2 jp] = first 4, acc[i][2 jp + 1]
 // = last 4).  Bias is loaded once; residual rows are fetched 4 row blocks at a time.
-template <int EPI, int DG = 0>
+template <int EPI, int DG = 0, typename PF = NoPF>
 __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int lane, int m_base,
                                                 int n_base, const EpiArgs& e,
-                                                const float2* lst = nullptr) {
+                                                const float2* lst = nullptr, PF pf = PF{}) {
   constexpr int ACT = EPI & 3;
   constexpr bool OUT_BF16 = (EPI & 4) != 0;
   constexpr bool RESID = (EPI & 8) != 0 && !(DG & 2);
@@ -685,16 +730,23 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
             n_base + 32 * jp + 8 * fg);
   };
   if constexpr (RPRE) load_raw(0, rraw[0]);
+  else pf();
 #pragma unroll
   for (int i0 = 0; i0 < 8; i0 += 4) {
     f32x4 rv[4][2][2];
     float2 st[4];                      // LayerNorm fold: the (mean, rstd) of rows 16 (i0 + i) + fr
-    if constexpr (LNF) {
+    if constexpr (LNF && !std::is_same<PF, NoPF>::value) {   // see epilogue_fast
+      if (i0 == 0) lds_read4_b64<0, 128, 256, 384>(lst + fr, st);
+      else lds_read4_b64<512, 640, 768, 896>(lst + fr, st);
+    } else if constexpr (LNF) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) st[i] = lst[16 * (i0 + i) + fr];
     }
     if constexpr (RPRE) {
-      if (i0 == 0) load_raw(4, rraw[1]);
+      if (i0 == 0) {
+        load_raw(4, rraw[1]);
+        pf();
+      }
     } else if constexpr (RESID) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -825,13 +877,18 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fg = lane >> 4;
   uint64_t ts[4] = {0, 0, 0, 0};
-  if constexpr ((DG & 16) != 0) ts[0] = __builtin_amdgcn_s_memtime();
+  [[maybe_unused]] uint64_t rt0 = 0;
+  if constexpr ((DG & 16) != 0) {
+    ts[0] = __builtin_amdgcn_s_memtime();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
   pp2_mainloop<TR>(acc, smem, src, nk, wave, wm, wn, fr, fg, (DG & 16) ? &ts[1] : nullptr);
   if constexpr ((DG & 16) != 0) ts[2] = __builtin_amdgcn_s_memtime();
   const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
 #if VTD_DIAG
   // DG & 16 (diagnostic build): per-workgroup s_memtime stamps of wave 0 -- start, prologue
-  // landed, main loop done, epilogue stores issued -- and the XCC id, at g_pp2_stamps[bid]
+  // landed, main loop done, epilogue stores issued -- and s_memrealtime (100 MHz) at the start
+  // and the end, at g_pp2_stamps[bid]
   auto stamp = [&]() {
     if constexpr ((DG & 16) != 0) {
       ts[3] = __builtin_amdgcn_s_memtime();
@@ -840,8 +897,8 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
         g_pp2_stamps[bid * 6 + 1] = ts[1];
         g_pp2_stamps[bid * 6 + 2] = ts[2];
         g_pp2_stamps[bid * 6 + 3] = ts[3];
-        g_pp2_stamps[bid * 6 + 4] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));
-        g_pp2_stamps[bid * 6 + 5] = (uint64_t)tile;
+        g_pp2_stamps[bid * 6 + 4] = rt0;
+        g_pp2_stamps[bid * 6 + 5] = __builtin_amdgcn_s_memrealtime();
       }
     }
   };
@@ -884,6 +941,124 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
     }
   }
   epilogue_generic(acc, ep, lane, M, N, m_base, n_base, e);
+}
+
+// Several tiles per workgroup (knob VTD_KNOB_GEMM_TPW > 1, the forward's epilogue codes):
+// pp2's K loop and epilogues in a tile loop; a tile's epilogue issues the next tile's first
+// K-stage into stage 0 (the epilogue's LDS lies past it), so that the next K loop starts on
+// landed operands, and the workgroup is not relaunched per tile.
+template <int EPI, bool TR>
+__global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_mt_kernel(
+    int M, int N, int K, const bf16_t* __restrict__ A, int lda,
+    const bf16_t* __restrict__ Bt, int ldb, int tiles_m, int tiles_n, EpiArgs e) {
+  constexpr int DG = 0;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane0 = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nt = tiles_m * tiles_n;
+  // the grid's nwg workgroups take tiles v, v + nwg, v + 2 nwg, ... (XCD-remapped v): the
+  // tiles in flight at any time are one contiguous range of the tile order, as in the
+  // one-tile launch (L2 reuse of the A / B panels)
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int v = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  int tile = v;
+  const int nk = K / 64, k0 = 0;
+  int tm, tn;
+  tile_coords(tile, tiles_m, tiles_n, e.ngw, tm, tn);
+  // epilogue LDS (32-row staging per wave, then the LayerNorm-fold statistics table) past
+  // stage 0: the next tile's first K-stage lands there during the epilogue
+  char* const epb = smem + BSTAGE;
+  uint64_t ts[4] = {0, 0, 0, 0};
+  [[maybe_unused]] uint64_t rt0 = 0;
+  if constexpr ((DG & 16) != 0) {
+    ts[0] = __builtin_amdgcn_s_memtime();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
+  bool pre = false;
+  for (;;) {
+    const int m0 = tm * BBM, n0 = tn * BBN;
+    // per-lane addressing is rederived inside each tile (the opaque copy of the lane id keeps
+    // the compiler from hoisting it out of the tile loop, where it would stay live through
+    // the epilogue), so a one-tile workgroup has the register budget of a loop-free kernel
+    int lane = lane0;
+    asm volatile("" : "+v"(lane));
+    const int fr = lane & 15, fg = lane >> 4;
+    float* const ep = reinterpret_cast<float*>(epb) + wave * 32 * 68;
+    float2* const lds_st = reinterpret_cast<float2*>(epb + 8 * 32 * 68 * 4) + wave * 128;
+    PP2BufSrc src;
+    pp2b_sources<TR>(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane, k0 * 64);
+    // LayerNorm-fold row statistics of the wave's 128 rows: issued before the K loop (older
+    // than the K loop's DMAs, so its counted waits retire them), used in the epilogue
+    float2 lst[2] = {float2{0.f, 0.f}, float2{0.f, 0.f}};
+    if constexpr (EPI != EPI_GENERIC && (EPI & EPI_LNF) != 0) {
+      lst[0] = e.lnstat[min(m0 + wm * 128 + lane, M - 1)];
+      lst[1] = e.lnstat[min(m0 + wm * 128 + 64 + lane, M - 1)];
+    }
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    pp2_mainloop<TR>(acc, smem, src, nk, wave, wm, wn, fr, fg,
+                     ((DG & 16) && !pre) ? &ts[1] : nullptr, pre);
+    if constexpr ((DG & 16) != 0) {
+      if (!pre) ts[2] = __builtin_amdgcn_s_memtime();
+    }
+    const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
+    // the statistics table (wave-private; the epilogues read a row's pair with a broadcast
+    // ds_read_b64, no lane shuffles)
+    if constexpr (EPI != EPI_GENERIC && (EPI & EPI_LNF) != 0) {
+      lds_st[lane] = lst[0];
+      lds_st[64 + lane] = lst[1];
+    }
+    // next tile of this workgroup: its K-tile 0 is loaded into stage 0 now (every wave has
+    // left the K loop: stages are free), under this tile's epilogue
+    const bool more = tile + nwg < nt;
+    int tm2 = tm, tn2 = tn;
+    if (more) tile_coords(tile + nwg, tiles_m, tiles_n, e.ngw, tm2, tn2);
+    // issued unconditionally (out-of-range, traffic-free loads after the last tile): the
+    // same instruction sequence on both paths keeps the compiler's counted waits for the
+    // epilogue's own loads exact, instead of the minimum over a branch merge
+    auto prefetch = [&]() {
+      PP2BufSrc nsrc;
+      pp2b_sources<TR>(nsrc, A, lda, M, Bt, ldb, N, tm2 * BBM, tn2 * BBN, wave, lane, k0 * 64,
+                       more);
+      pp2_issue<0>(smem, nsrc, wave, 0, 0);
+      pp2_issue<2>(smem, nsrc, wave, 0, 0);
+      pp2_issue<3>(smem, nsrc, wave, 0, 0);
+      pp2_issue<1>(smem, nsrc, wave, 0, 0);
+    };
+    if constexpr ((DG & 8) != 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+      prefetch();
+    } else {
+      bool done = false;
+      if constexpr (EPI != EPI_GENERIC) {
+        if (m0 + BBM <= M && n0 + BBN <= N) {
+          if constexpr (TR) epilogue_direct<EPI, DG>(acc, lane, m_base, n_base, e, lds_st, prefetch);
+          else epilogue_fast<EPI, 32, DG>(acc, ep, lane, m_base, n_base, e, lds_st, prefetch);
+          done = true;
+        }
+      }
+      if (!done) {
+        prefetch();
+        if constexpr (TR) epilogue_direct_generic(acc, ep, lane, M, N, m_base, n_base, e);
+        else epilogue_generic(acc, ep, lane, M, N, m_base, n_base, e);
+      }
+    }
+    if (!more) break;
+    tile += nwg;
+    tm = tm2;
+    tn = tn2;
+    pre = true;
+  }
 }
 
 // The fp32 parity mode's 256 x 256-tile kernel: pp2's staging, ping-pong schedule and
@@ -1245,10 +1420,34 @@ bool gemm_mx8_emits_fp8(int M, int N, const vtd_epilogue* e) {
 int ln_stats_finalize_launch(const float* part, int64_t rows, int slots, int D, float eps,
                              float* stat, hipStream_t st);
 
+// multi-tile pp2 dynamic LDS: stage 0, then stage 1 overlapped by the epilogue staging and
+// the statistics table (stage 0 takes the next tile's first K-stage during an epilogue)
+constexpr size_t kPP2LdsMax = BSTAGE + 8 * 32 * 68 * 4 + 8 * 128 * 8;
+static_assert(kPP2LdsMax <= 160 * 1024 && kPP2LdsMax >= 2 * BSTAGE, "pp2 LDS");
+// the epilogue codes with a multi-tile kernel: the forward's query/key/value and mlp1
+// (LayerNorm fold), attention_output / mlp3 (residual + statistics), mlp2
+constexpr bool pp2_mt_code(int c) {
+  return c == (4 | EPI_LNF) || c == (5 | EPI_LNF) || c == (12 | EPI_STAT) || c == 5 || c == 12;
+}
+// tiles per pp2 workgroup (knob VTD_KNOB_GEMM_TPW)
+inline int pp2_tpw() { return std::max(1, knob(VTD_KNOB_GEMM_TPW)); }
+
 template <int C>
 void pp2_launch(bool tr, dim3 g, hipStream_t stream, int M, int N, int K, const bf16_t* A, int lda,
                 const bf16_t* Bt, int ldb, int tiles_m, int tiles_n, const EpiArgs& e,
                 int ksplit = 1) {
+  if constexpr (pp2_mt_code(C)) {
+    if (ksplit == 1 && e.tpw > 1) {
+      const dim3 gm((tiles_m * tiles_n + e.tpw - 1) / e.tpw);
+      if (tr)
+        hipLaunchKernelGGL((gemm_tn_bf16_pp2_mt_kernel<C, true>), gm, dim3(BNT), kPP2LdsMax,
+                           stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
+      else
+        hipLaunchKernelGGL((gemm_tn_bf16_pp2_mt_kernel<C, false>), gm, dim3(BNT), kPP2LdsMax,
+                           stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e);
+      return;
+    }
+  }
   if (tr)
     hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, true>), g, dim3(BNT), 2 * BSTAGE, stream, M,
                        N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e, ksplit);
@@ -1266,6 +1465,13 @@ void pp2_set_attributes() {
 #undef VTD_PP_FN
     for (const void* f : fns)
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
+#define VTD_MT_FN(C) reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_mt_kernel<C, false>), \
+                     reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_mt_kernel<C, true>),
+    const void* mts[] = {VTD_MT_FN(4 | EPI_LNF) VTD_MT_FN(5 | EPI_LNF) VTD_MT_FN(12 | EPI_STAT)
+                         VTD_MT_FN(5) VTD_MT_FN(12)};
+#undef VTD_MT_FN
+    for (const void* f : mts)
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPP2LdsMax);
   });
 }
 
@@ -1303,6 +1509,13 @@ void f32_pp2_launch(int M, int N, int K, const float* A, int lda, const float* B
 #undef VTD_F32_FN
     for (const void* f : fns)
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
+#define VTD_MT_FN(C) reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_mt_kernel<C, false>), \
+                     reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_mt_kernel<C, true>),
+    const void* mts[] = {VTD_MT_FN(4 | EPI_LNF) VTD_MT_FN(5 | EPI_LNF) VTD_MT_FN(12 | EPI_STAT)
+                         VTD_MT_FN(5) VTD_MT_FN(12)};
+#undef VTD_MT_FN
+    for (const void* f : mts)
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPP2LdsMax);
   });
   EpiArgs e = make_epi_args(epi);
   e.ngw = tile_group_width(tiles_n);
@@ -1388,6 +1601,7 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
     pp2_set_attributes();
     EpiArgs e = make_epi_args(epi);
     e.ngw = ngw;
+    e.tpw = pp2_tpw();
     const int code = pp2_code(epi);
     // transposed accumulators + register-direct epilogue for activation layers (mlp1 -5 %,
     // mlp2 -1.5 %), LDS-staged row vectors for the others (attn_out -10 %, mlp3 -4 %);
@@ -1396,6 +1610,7 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
     const bool tr = ktr >= 0 ? ktr != 0 : e.act != VTD_ACT_NONE;
     const dim3 g(tiles_m * tiles_n);
 #if VTD_DIAG
+    const size_t lds = 2 * BSTAGE;
     // epilogue ablation (wrong outputs): VTD_PP2_DG = the DG bits of epilogue_fast /
     // epilogue_direct, for the plain / residual / statistics codes gemm_bench uses
     static const int pp2_dg = getenv("VTD_PP2_DG") ? atoi(getenv("VTD_PP2_DG")) : 0;
@@ -1419,9 +1634,9 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
         });
 #define VTD_DG_L(D)                                                                                \
   if (pp2_dg == D) {                                                                               \
-    if (tr) hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, true, D>), g, dim3(BNT), 2 * BSTAGE,    \
+    if (tr) hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, true, D>), g, dim3(BNT), lds,           \
                                stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e, 1);       \
-    else hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, false, D>), g, dim3(BNT), 2 * BSTAGE,      \
+    else hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, false, D>), g, dim3(BNT), lds,             \
                             stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e, 1);          \
   }
         VTD_DG_L(1) VTD_DG_L(2) VTD_DG_L(4) VTD_DG_L(8) VTD_DG_L(16)

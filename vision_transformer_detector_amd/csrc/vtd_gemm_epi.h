@@ -37,6 +37,9 @@ struct EpiArgs {
   // split-K partial launches (pp2, ksplit > 1): split s writes its fp32 partial tile at
   // out + s * split_stride (elements)
   int64_t split_stride;
+  // pp2 (ksplit == 1): consecutive tiles per workgroup (<= 1: one); with more than one, the
+  // next tile's first K-stage is loaded while the current tile's epilogue runs
+  int tpw;
 };
 
 // bf16 output row vector store of the fast epilogues; build-time A/B knob VTD_OUT_NT: 1 =

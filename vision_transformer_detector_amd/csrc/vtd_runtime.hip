@@ -59,7 +59,8 @@ namespace {
 constexpr const char* kKnobEnv[VTD_KNOB_COUNT] = {"VTD_ATTN_VARIANT", "VTD_ATTN_GRID",
                                                   "VTD_GEMM_NGW", "VTD_SPLITK",
                                                   "VTD_JPEG_CHUNK_BITS", "VTD_SKINNY",
-                                                  "VTD_F32_PP2", "VTD_STAGGER", "VTD_GEMM_TR"};
+                                                  "VTD_F32_PP2", "VTD_STAGGER", "VTD_GEMM_TR",
+                                                  "VTD_FIN_WGS", "VTD_GEMM_TPW"};
 std::atomic<int> g_knob[VTD_KNOB_COUNT];
 std::once_flag g_knob_once;
 void knob_init() {
