@@ -304,10 +304,11 @@ int vtd_resize_with_pad(const uint8_t* pixels_dev, const int64_t* offsets_dev,
 
 /* JPEG decode on the device, tf.image.decode_image(file, channels=3)
  * (vision_transformer_utilities.py:431) for baseline / extended sequential and progressive
- * Huffman JPEG: 8-bit, 1 or 3 components, 4:4:4 / 4:2:2 / 4:2:0, restart intervals.
- * libjpeg-turbo's decode path (what TF uses): ISLOW IDCT, fancy upsampling, YCbCr -> RGB;
- * gray -> RGB replicated.  Other JPEGs (arithmetic-coded, lossless, 12-bit, 4:4:0, ...)
- * return VTD_ERR_UNSUPPORTED with the reason.
+ * Huffman JPEG: 8-bit, 1, 3 or 4 (CMYK / YCCK) components, 4:4:4 / 4:2:2 / 4:2:0, restart
+ * intervals.  libjpeg-turbo's decode path (what TF uses): ISLOW IDCT, fancy upsampling,
+ * YCbCr -> RGB; gray -> RGB replicated; CMYK (YCCK -> CMYK as jdcolor.c) -> RGB as TF's
+ * jpeg_mem.cc (Adobe marker: R = K C / 255, else (255 - K)(255 - C) / 255).  Other JPEGs
+ * (arithmetic-coded, lossless, 12-bit, 4:4:0, ...) return VTD_ERR_UNSUPPORTED with the reason.
  * vtd_jpeg_info: header only (host).  The images are HOST buffers; their marker segments are
  * parsed on the host, the entropy-coded data + derived tables copied to the workspace on
  * `stream` (through a pinned staging buffer the library reuses), image i written as RGB

@@ -159,3 +159,74 @@ def test_jpeg_unsupported_raises(cuda):
         decode_jpegs([cmyk], device=cuda)
     with pytest.raises(ValueError):
         decode_jpegs([b"\x00\x01not a jpeg"], device=cuda)
+
+
+def _cmyk_image(h, w, seed):
+    """Four independent smooth + noisy channels (K not derived from C, M, Y)."""
+    rgb = _image(h, w, seed)
+    k = _image(h, w, seed + 1000)[..., 0]
+    return np.concatenate([rgb, k[..., None]], -1)
+
+
+def _cmyk_file(h, w, seed, **kw):
+    b = io.BytesIO()
+    Image.fromarray(_cmyk_image(h, w, seed), mode="CMYK").save(b, format="JPEG", **kw)
+    return b.getvalue()
+
+
+def _adobe_transform(data, t):
+    """The same file with its Adobe APP14 transform byte set to t (2: YCCK -- libjpeg then
+    converts the first three planes from YCbCr; the coefficients stay valid)."""
+    i = data.index(b"Adobe") - 4
+    assert data[i:i + 2] == b"\xff\xee"
+    return data[:i + 4 + 11] + bytes([t]) + data[i + 4 + 12:]
+
+
+def _without_adobe(data):
+    i = data.index(b"Adobe") - 4
+    ln = int.from_bytes(data[i + 2:i + 4], "big")
+    return data[:i] + data[i + 2 + ln:]
+
+
+def _tf_cmyk_rgb(data):
+    """Expected `decode_image(f, channels=3)` of a 4-component JPEG: libjpeg-turbo's CMYK
+    output (Pillow's CMYK pixels are its inversion, rawmode "CMYK;I"), then TF's
+    jpeg_mem.cc CMYK -> RGB (integer division; Adobe marker: R = K C / 255, otherwise
+    R = (255 - K)(255 - C) / 255)."""
+    im = Image.open(io.BytesIO(data))
+    assert im.mode == "CMYK"
+    raw = 255 - np.asarray(im).astype(np.int64)
+    c, m, y, k = (raw[..., i] for i in range(4))
+    if b"Adobe" in data:
+        out = np.stack([k * c // 255, k * m // 255, k * y // 255], -1)
+    else:
+        out = np.stack([(255 - k) * (255 - c) // 255, (255 - k) * (255 - m) // 255,
+                        (255 - k) * (255 - y) // 255], -1)
+    return out.astype(np.uint8)
+
+
+def test_jpeg_cmyk_and_ycck_vs_libjpeg_turbo(cuda):
+    """4-component JPEGs: the CMYK planes are libjpeg-turbo's bit for bit
+    (Pillow's decode: baseline, progressive, 4:2:0-sampled first plane, an Adobe transform 2
+    file that libjpeg decodes as YCCK through jdcolor.c ycck_cmyk_convert, a file without the
+    Adobe marker), and the RGB is TF's CMYK -> RGB of those planes (restated from TF's
+    jpeg_mem.cc; TF itself is not importable, so that last integer step is unpinned)."""
+    from vision_transformer_detector_amd.preprocess import decode_jpegs
+    base = _cmyk_file(37, 53, 1, quality=90)
+    files = [base, _cmyk_file(48, 64, 2, quality=75, subsampling=2),
+             _cmyk_file(61, 45, 3, quality=85, progressive=True),
+             _cmyk_file(1, 1, 4, quality=80),
+             _adobe_transform(base, 2), _without_adobe(base),
+             _encode(_image(20, 24, 5), quality=85, subsampling=2)]     # + an RGB file
+    assert b"Adobe" in base and b"\xff\xc2" in files[2]
+    pixels, offsets, sizes = decode_jpegs(files, device=cuda)
+    torch.cuda.synchronize()
+    got = pixels.cpu().numpy()
+    for i, f in enumerate(files):
+        ref = _tf_cmyk_rgb(f) if i < len(files) - 1 else _pil_rgb(f)
+        h, w = sizes[i]
+        assert (h, w) == ref.shape[:2]
+        mine = got[offsets[i]:offsets[i] + h * w * 3].reshape(h, w, 3)
+        bad = np.argwhere(mine != ref)
+        assert bad.size == 0, (f"file {i}: {len(bad)} differing values, first at "
+                               f"{bad[0].tolist()}: {mine[tuple(bad[0])]} vs {ref[tuple(bad[0])]}")

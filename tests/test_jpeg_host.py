@@ -77,10 +77,14 @@ def test_workspace_plan_dims_and_growth(L):
 
 
 def test_unsupported_flavours_name_the_reason(L):
-    cmyk = _jpeg(16, 16, "CMYK", quality=80)
-    rc, _ = _info(L, cmyk)
+    # two components: the RGB file's frame header with Nf = 2
+    rgb = _jpeg(16, 16, quality=80)
+    i = rgb.index(b"\xff\xc0")
+    assert rgb[i + 9] == 3
+    two = rgb[:i + 9] + b"\x02" + rgb[i + 10:]
+    rc, _ = _info(L, two)
     assert rc != 0 and b"component" in L.lib.vtd_last_error()
-    rc, _, _ = _plan(L, [_jpeg(8, 8), cmyk])
+    rc, _, _ = _plan(L, [_jpeg(8, 8), two])
     assert rc != 0 and b"image 1" in L.lib.vtd_last_error()
     # arithmetic coding (SOF9): the same file with its SOF0 marker byte changed
     base = _jpeg(16, 16, quality=80)
@@ -173,3 +177,13 @@ def test_decode_requires_a_hip_device():
     from vision_transformer_detector_amd.preprocess import decode_jpegs
     with pytest.raises(ValueError, match="HIP device"):
         decode_jpegs([_jpeg(8, 8)], device="cpu")
+
+
+def test_cmyk_header_walk(L):
+    """4-component (CMYK; Adobe APP14) JPEGs pass the header walk with comps = 4."""
+    cmyk = _jpeg(16, 24, "CMYK", quality=80)
+    assert b"Adobe" in cmyk
+    rc, dims = _info(L, cmyk)
+    assert rc == 0 and dims == (16, 24, 4), dims
+    rc, pd, ws = _plan(L, [_jpeg(8, 8), cmyk])
+    assert rc == 0 and ws > 0

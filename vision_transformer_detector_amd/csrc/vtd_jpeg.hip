@@ -1,7 +1,7 @@
 // JPEG decode on the device: the first step of the reference's input pipeline,
 // `tf.image.decode_image(image_file, channels=3)` (vision_transformer_utilities.py:431),
-// for baseline JPEG (sequential Huffman, 8-bit, 1 or 3 components, 4:4:4 / 4:2:2 / 4:2:0,
-// restart intervals).  TF decodes JPEG with libjpeg-turbo (default INTEGER_ISLOW IDCT,
+// for baseline JPEG (sequential Huffman, 8-bit, 1, 3 or 4 (CMYK / YCCK) components,
+// 4:4:4 / 4:2:2 / 4:2:0, restart intervals).  TF decodes JPEG with libjpeg-turbo (default INTEGER_ISLOW IDCT,
 // fancy upsampling); this restates that library's decode path exactly:
 //   - entropy decoding as jdhuff.c decode_mcu (DC prediction per component, HUFF_EXTEND,
 //     restart markers reset the predictions);
@@ -42,7 +42,8 @@ namespace vtd {
 
 namespace {
 
-constexpr int kMaxComp = 3;
+constexpr int kMaxComp = 4;        // Y / YCbCr / CMYK or YCCK
+constexpr int kScanV = 1 + kMaxComp;  // segmented scan lanes: blocks + DC per component
 
 struct JpegComp {
   int id;                   // component identifier of the frame header (scans name it)
@@ -55,6 +56,8 @@ struct JpegComp {
 
 struct JpegDesc {
   int h, w, nc, mcux, mcuy, hmax, vmax, restart, rgb;   // rgb: Adobe transform 0 (no YCC)
+  int adobe;                // an Adobe APP14 marker was seen (CMYK polarity, see pixel_rgb)
+  int ycck;                 // 4 components coded as YCCK (Adobe transform != 0)
   int nblocks;              // blocks of all components
   int64_t coef_base;        // first block of this image in the coefficient buffer
   int64_t data_off;         // entropy-coded segment in the packed data buffer
@@ -263,8 +266,8 @@ bool parse_jpeg(const uint8_t* b, size_t n, JpegDesc& d, size_t& seg, size_t& se
       d.w = u16(s + 3);
       d.nc = b[s + 5];
       if (d.h <= 0 || d.w <= 0) { err = "jpeg: bad frame size (DNL not supported)"; return false; }
-      if (!(d.nc == 1 || d.nc == 3) || len != 8 + 3 * d.nc) {
-        err = "jpeg: only 1- or 3-component images are supported";
+      if (!(d.nc == 1 || d.nc == 3 || d.nc == 4) || len != 8 + 3 * d.nc) {
+        err = "jpeg: only 1-, 3- or 4-component images are supported";
         return false;
       }
       for (int c = 0; c < d.nc; ++c) {
@@ -320,7 +323,11 @@ bool parse_jpeg(const uint8_t* b, size_t n, JpegDesc& d, size_t& seg, size_t& se
       if (len < 4) { err = "jpeg: truncated DRI segment"; return false; }
       d.restart = u16(s);
     } else if (m == 0xEE && len >= 14 && !memcmp(b + s, "Adobe", 5)) {
-      d.rgb = b[s + 11] == 0 ? 1 : 0;                         // transform 0: RGB / no YCC
+      // jdmarker.c get_interesting_appn / jdapimin.c default_decompress_parms: transform 0
+      // = RGB (3 components) / CMYK (4); otherwise YCbCr / YCCK
+      d.adobe = 1;
+      d.rgb = b[s + 11] == 0 ? 1 : 0;
+      d.ycck = b[s + 11] != 0 ? 1 : 0;
     } else if (m == 0xDA) {                                   // SOS
       if (!frame) { err = "jpeg: scan before frame"; return false; }
       if (len < 3) { err = "jpeg: truncated SOS segment"; return false; }
@@ -632,7 +639,7 @@ __global__ __launch_bounds__(kThreads) void jpeg_huffman_kernel(const JpegDesc* 
   __shared__ HuffTables T;
   __shared__ uint64_t tail[2][kThreads];
   __shared__ int scan_f[kThreads];
-  __shared__ int scan_v[4][kThreads];
+  __shared__ int scan_v[kScanV][kThreads];
   const JpegDesc& d = descs[blockIdx.x];
   const int t = threadIdx.x;
   for (int i = t; i < 8 * 512; i += kThreads) (&T.lut[0][0])[i] = (&d.lut[0][0])[i];
@@ -702,37 +709,38 @@ __global__ __launch_bounds__(kThreads) void jpeg_huffman_kernel(const JpegDesc* 
     if (!__syncthreads_or(changed)) break;
   }
 
-  // ---- count: segmented exclusive scan of (blocks, dc[0..2]) over the chunks
-  int f = 0, v[4] = {0, 0, 0, 0};
+  // ---- count: segmented exclusive scan of (blocks, dc[0..kMaxComp-1]) over the chunks
+  int f = 0, v[kScanV] = {};
   for (int c = c0; c < c1; ++c) {
     if (chunks[c].flags & 1) {
       f = 1;
-      v[0] = v[1] = v[2] = v[3] = 0;
+      for (int i = 0; i < kScanV; ++i) v[i] = 0;
     }
     v[0] += S[c].blocks;
     for (int i = 0; i < kMaxComp; ++i) v[1 + i] += S[c].dc[i];
   }
   scan_f[t] = f;
-  for (int i = 0; i < 4; ++i) scan_v[i][t] = v[i];
+  for (int i = 0; i < kScanV; ++i) scan_v[i][t] = v[i];
   __syncthreads();
   for (int o = 1; o < kThreads; o <<= 1) {       // Hillis-Steele, inclusive
-    int pf = 0, pv[4] = {0, 0, 0, 0};
+    int pf = 0, pv[kScanV] = {};
     if (t >= o) {
       pf = scan_f[t - o];
-      for (int i = 0; i < 4; ++i) pv[i] = scan_v[i][t - o];
+      for (int i = 0; i < kScanV; ++i) pv[i] = scan_v[i][t - o];
     }
     __syncthreads();
     if (t >= o && !scan_f[t]) {
       scan_f[t] = pf;
-      for (int i = 0; i < 4; ++i) scan_v[i][t] += pv[i];
+      for (int i = 0; i < kScanV; ++i) scan_v[i][t] += pv[i];
     }
     __syncthreads();
   }
-  int run[4] = {0, 0, 0, 0};
+  int run[kScanV] = {};
   if (t > 0)
-    for (int i = 0; i < 4; ++i) run[i] = scan_v[i][t - 1];
+    for (int i = 0; i < kScanV; ++i) run[i] = scan_v[i][t - 1];
   for (int c = c0; c < c1; ++c) {
-    if (chunks[c].flags & 1) run[0] = run[1] = run[2] = run[3] = 0;
+    if (chunks[c].flags & 1)
+      for (int i = 0; i < kScanV; ++i) run[i] = 0;
     S[c].bpre = run[0];
     for (int i = 0; i < kMaxComp; ++i) S[c].dpre[i] = run[1 + i];
     run[0] += S[c].blocks;
@@ -1099,7 +1107,13 @@ __device__ __forceinline__ int upsample(const uint8_t* p, int st, int dw, int dh
   return (cs * 3 + (r0[j + 1] * 3 + r1[j + 1]) + 7) >> 4;
 }
 
-// RGB of pixel (y, x): upsampled chroma + jdcolor.c ycc_rgb_convert (SCALEBITS 16)
+// RGB of pixel (y, x): upsampled chroma + jdcolor.c ycc_rgb_convert (SCALEBITS 16).
+// Four components: libjpeg's CMYK output (CMYK as coded, or YCCK through jdcolor.c
+// ycck_cmyk_convert: C, M, Y = 255 - the YCbCr -> RGB of the first three, K unchanged), then
+// the CMYK -> RGB of TF's decoder for a 3-channel request (tensorflow/core/lib/jpeg/
+// jpeg_mem.cc, UncompressLow; TF is not in this image, so that last step is restated, not
+// pinned): with an Adobe marker (inverted CMYK) R = K C / 255, else R = (255 - K)(255 - C) / 255,
+// integer division, likewise G from M and B from Y.
 __device__ __forceinline__ uchar3 pixel_rgb(const JpegDesc& d, const uint8_t* planes, int y, int x) {
   const JpegComp& c0 = d.comp[0];
   const int Y = planes[c0.plane_off + (int64_t)y * c0.bw * 8 + x];
@@ -1109,13 +1123,27 @@ __device__ __forceinline__ uchar3 pixel_rgb(const JpegDesc& d, const uint8_t* pl
                           d.comp[1].dh, hf, vf, y, x);
   const int cr = upsample(planes + d.comp[2].plane_off, d.comp[2].bw * 8, d.comp[2].dw,
                           d.comp[2].dh, hf, vf, y, x);
-  if (d.rgb) return make_uchar3(Y, cb, cr);
-  const int xcr = cr - 128, xcb = cb - 128;
-  const int cr_r = (91881 * xcr + 32768) >> 16;                     // FIX(1.40200)
-  const int cb_b = (116130 * xcb + 32768) >> 16;                    // FIX(1.77200)
-  const int cg = (-46802 * xcr + (-22554 * xcb + 32768)) >> 16;     // FIX(0.71414), FIX(0.34414)
-  return make_uchar3(min(max(Y + cr_r, 0), 255), min(max(Y + cg, 0), 255),
-                     min(max(Y + cb_b, 0), 255));
+  int r = Y, g = cb, b = cr;
+  if ((d.nc == 3 && !d.rgb) || (d.nc == 4 && d.ycck)) {
+    const int xcr = cr - 128, xcb = cb - 128;
+    const int cr_r = (91881 * xcr + 32768) >> 16;                     // FIX(1.40200)
+    const int cb_b = (116130 * xcb + 32768) >> 16;                    // FIX(1.77200)
+    const int cg = (-46802 * xcr + (-22554 * xcb + 32768)) >> 16;     // FIX(0.71414), FIX(0.34414)
+    r = min(max(Y + cr_r, 0), 255);
+    g = min(max(Y + cg, 0), 255);
+    b = min(max(Y + cb_b, 0), 255);
+  }
+  if (d.nc == 3) return make_uchar3(r, g, b);
+  const int k = upsample(planes + d.comp[3].plane_off, d.comp[3].bw * 8, d.comp[3].dw,
+                         d.comp[3].dh, hf, vf, y, x);
+  if (d.ycck) {                                       // ycck_cmyk_convert
+    r = 255 - r;
+    g = 255 - g;
+    b = 255 - b;
+  }
+  if (d.adobe) return make_uchar3(k * r / 255, k * g / 255, k * b / 255);
+  return make_uchar3((255 - k) * (255 - r) / 255, (255 - k) * (255 - g) / 255,
+                     (255 - k) * (255 - b) / 255);
 }
 
 // One workgroup per (row segment of kColorSeg pixels, row, image): the segment's RGB bytes

@@ -69,8 +69,9 @@ def decode_jpegs(files, device="cuda", stream=None):
     """JPEG file bytes (a list of `bytes`) -> (packed RGB uint8 pixels on `device`, per-image
     byte offsets (int64, host), [(height, width), ...]): `tf.image.decode_image(f, channels=3)`
     (vision_transformer_utilities.py:431) for baseline / extended sequential and progressive
-    Huffman JPEGs, decoded on the device by vtd_jpeg_decode.  Unsupported JPEG flavours
-    (arithmetic-coded, lossless, 12-bit, 4:4:0, CMYK / YCCK) raise ValueError naming the
+    Huffman JPEGs (1, 3 or 4 -- CMYK / YCCK -- components), decoded on the device by
+    vtd_jpeg_decode.  Unsupported JPEG flavours
+    (arithmetic-coded, lossless, 12-bit, 4:4:0) raise ValueError naming the
     reason; nothing falls back to a host decoder."""
     import ctypes
     if len(files) == 0:
