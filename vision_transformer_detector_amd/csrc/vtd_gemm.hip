@@ -265,7 +265,11 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
   constexpr bool NOBIAS = (EPI & EPI_PARTIAL) != 0;   // split-K partial: raw fp32 sums
   constexpr bool LNF = (EPI & EPI_LNF) != 0, STAT = (EPI & EPI_STAT) != 0 && !(DG & 1);
   constexpr bool F8O = (EPI & EPI_F8O) != 0;
-  constexpr int ES = 68;
+  // staging image: 64-float rows, 16-B chunk c of row r at chunk c ^ (r & 7) -- conflict-free
+  // for both the ds_write_b32 scatter of the accumulators and the ds_read_b128 row reads
+  // (a 68-float pitch left the reads 2-way conflicted: SQ_LDS_BANK_CONFLICT ~20 % of the
+  // LDS cycles of the query/key/value and attention-output kernels)
+  auto sidx = [](int row, int col) { return row * 64 + (((col >> 2) ^ (row & 7)) << 2) + (col & 3); };
   constexpr int NB = PR / 16;            // accumulator row blocks per pass
   constexpr int NIT = PR / 8;            // row-vector iterations per pass
   const int fr = lane & 15, fg = lane >> 4;
@@ -303,7 +307,7 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r2 = 0; r2 < 4; ++r2)
-          ep[(i * 16 + fg * 4 + r2) * ES + j * 16 + fr] = acc[p * NB + i][j][r2];
+          ep[sidx(i * 16 + fg * 4 + r2, j * 16 + fr)] = acc[p * NB + i][j][r2];
     if constexpr (RPRE) {
       if (p + 1 < 128 / PR) load_raw(p + 1, rraw[(p + 1) & 1]);
       if (p == 0) pf();
@@ -330,8 +334,8 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
       const int row = it * 8 + rsub;
-      f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + row * ES + c8);
-      f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + row * ES + c8 + 4);
+      f32x4 v0 = *reinterpret_cast<const f32x4*>(ep + sidx(row, c8));
+      f32x4 v1 = *reinterpret_cast<const f32x4*>(ep + sidx(row, c8 + 4));
       if constexpr (ASM_ST) epi_lnfold8_st(stv[it], cs0, cs1, v0, v1);
       else if constexpr (LNF) epi_lnfold8_st(lst[p * PR + row], cs0, cs1, v0, v1);
       v0 += b0;
