@@ -154,9 +154,11 @@ def test_jpeg_decode_then_resize_matches_host_pipeline(cuda):
 
 def test_jpeg_unsupported_raises(cuda):
     from vision_transformer_detector_amd.preprocess import decode_jpegs
-    cmyk = _encode(_image(40, 40, 1), "CMYK", quality=80)
+    rgb = _encode(_image(40, 40, 1), quality=80)
+    i = rgb.index(b"\xff\xc0")
+    two = rgb[:i + 9] + b"\x02" + rgb[i + 10:]          # Nf = 2: no such colour space
     with pytest.raises(ValueError, match="component"):
-        decode_jpegs([cmyk], device=cuda)
+        decode_jpegs([two], device=cuda)
     with pytest.raises(ValueError):
         decode_jpegs([b"\x00\x01not a jpeg"], device=cuda)
 

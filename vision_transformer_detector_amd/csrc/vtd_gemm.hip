@@ -211,6 +211,9 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(int M, int N, int K,
 }
 
 constexpr int BBM = 256, BBN = 256, BNT = 512;
+#ifndef VTD_TRS
+#define VTD_TRS 0
+#endif
 constexpr int BSTAGE = (BBM + BBN) * KB;     // 64 KiB per stage
 static_assert(8 * 32 * 68 * 4 + 8 * 128 * 8 <= 2 * BSTAGE,
               "epilogue staging + LayerNorm-fold row tables must fit the stages");
@@ -255,7 +258,9 @@ __device__ __forceinline__ void lds_read4_b64(const void* p, float2 (&o)[4]) {
       : "v"(a), "i"(O0), "i"(O1), "i"(O2), "i"(O3)
       : "memory");
 }
-template <int EPI, int PR = 32, int DG = 0, typename PF = NoPF>
+// TRL: the accumulators are in the transposed layout (lane (fr, fg): row 16 i + fr, columns
+// 32 jp + 8 fg .. + 7 in acc[i][2 jp], acc[i][2 jp + 1]): staged with ds_write_b128
+template <int EPI, int PR = 32, int DG = 0, typename PF = NoPF, bool TRL = false>
 __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* ep, int lane,
                                               int m_base, int n_base, const EpiArgs& e,
                                               const float2* lst = nullptr, PF pf = PF{}) {
@@ -301,13 +306,22 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
   else pf();
 #pragma unroll
   for (int p = 0; p < 128 / PR; ++p) {
+    if constexpr (TRL) {
 #pragma unroll
-    for (int i = 0; i < NB; ++i)
+      for (int i = 0; i < NB; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+        for (int jj = 0; jj < 4; ++jj)
+          *reinterpret_cast<f32x4*>(ep + sidx(i * 16 + fr, 32 * (jj >> 1) + 8 * fg + 4 * (jj & 1))) =
+              acc[p * NB + i][jj];
+    } else {
 #pragma unroll
-        for (int r2 = 0; r2 < 4; ++r2)
-          ep[sidx(i * 16 + fg * 4 + r2, j * 16 + fr)] = acc[p * NB + i][j][r2];
+      for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r2 = 0; r2 < 4; ++r2)
+            ep[sidx(i * 16 + fg * 4 + r2, j * 16 + fr)] = acc[p * NB + i][j][r2];
+    }
     if constexpr (RPRE) {
       if (p + 1 < 128 / PR) load_raw(p + 1, rraw[(p + 1) & 1]);
       if (p == 0) pf();
@@ -927,7 +941,13 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
   if constexpr (TR) {
     if constexpr (EPI != EPI_GENERIC) {
       if (m0 + BBM <= M && n0 + BBN <= N) {
-        epilogue_direct<EPI, DG>(acc, lane, m_base, n_base, e, lds_st);
+        // VTD_TRS (A/B builds): the transposed accumulators staged through LDS by 16-B writes
+        // and stored as whole-line row vectors (epilogue_fast) instead of register-direct
+        if constexpr (VTD_TRS && (EPI & 4) != 0 && (EPI & EPI_F8O) == 0)
+          epilogue_fast<EPI, 32, DG, NoPF, true>(acc, reinterpret_cast<float*>(smem) + wave * 32 * 68,
+                                                 lane, m_base, n_base, e, lds_st);
+        else
+          epilogue_direct<EPI, DG>(acc, lane, m_base, n_base, e, lds_st);
         stamp();
         return;
       }
@@ -1057,7 +1077,12 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_mt_kernel(
         else epilogue_generic(acc, ep, lane, M, N, m_base, n_base, e);
       }
     }
-    if (!more) break;
+    if (!more) {
+      // the last epilogue issued traffic-free out-of-range DMAs into stage 0: drain them
+      // before the workgroup (and its LDS allocation) ends
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      break;
+    }
     tile += nwg;
     tm = tm2;
     tn = tn2;
