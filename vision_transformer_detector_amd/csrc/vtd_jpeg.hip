@@ -548,28 +548,30 @@ __device__ __forceinline__ int huff_extend(int x, int s) {
   return x < (1 << (s - 1)) ? x + (-1 << s) + 1 : x;
 }
 
-// Three per-component counters kept in registers (a dynamically indexed array would live
-// in scratch memory).
-struct Comp3 {
-  int a, b, c;
-  __device__ void set(int v0, int v1, int v2) { a = v0; b = v1; c = v2; }
+// Per-component counters (kMaxComp = 4) kept in registers (a dynamically indexed array
+// would live in scratch memory).
+struct Comp4 {
+  int a, b, c, d;
+  __device__ void set(int v0, int v1, int v2, int v3) { a = v0; b = v1; c = v2; d = v3; }
   __device__ int add(int i, int v) {         // returns the new value of counter i
     a += i == 0 ? v : 0;
     b += i == 1 ? v : 0;
     c += i == 2 ? v : 0;
-    return i == 0 ? a : i == 1 ? b : c;
+    d += i == 3 ? v : 0;
+    return i == 0 ? a : i == 1 ? b : i == 2 ? c : d;
   }
 };
+static_assert(kMaxComp == 4, "Comp4 holds one counter per component");
 
 struct Decoder {
   Bits br;
   int u, k;
   int blocks;                     // blocks started since the chunk's start
-  Comp3 dc;                       // DC differences since the chunk's start
+  Comp4 dc;                       // DC differences since the chunk's start
   // write mode
   int16_t* blk;                   // current block (null: not writable)
   int q;                          // segment-relative number of the current block
-  Comp3 pred;
+  Comp4 pred;
 };
 
 // Block q of the segment starting at MCU `first_mcu`: its coefficient row.
@@ -626,7 +628,7 @@ __device__ uint64_t decode_chunk_count(Decoder& D, const JpegDesc& d, const Huff
   D.u = (int)(st >> 8) & 0xFF;
   D.k = (int)st & 0xFF;
   D.blocks = 0;
-  D.dc.set(0, 0, 0);
+  D.dc.set(0, 0, 0, 0);
   while (D.br.pos() < ch.end_bit) decode_symbol<false>(D, d, T, nullptr, ch);
   return pack_state(D.br.pos(), D.u, D.k);
 }
@@ -681,6 +683,7 @@ __global__ __launch_bounds__(kThreads) void jpeg_huffman_kernel(const JpegDesc* 
       S[c].dc[0] = D.dc.a;
       S[c].dc[1] = D.dc.b;
       S[c].dc[2] = D.dc.c;
+      S[c].dc[3] = D.dc.d;
     }
     tail[0][t] = st;
   }
@@ -701,6 +704,7 @@ __global__ __launch_bounds__(kThreads) void jpeg_huffman_kernel(const JpegDesc* 
           S[c].dc[0] = D.dc.a;
           S[c].dc[1] = D.dc.b;
           S[c].dc[2] = D.dc.c;
+          S[c].dc[3] = D.dc.d;
           if (c == c1 - 1) last = st;
         }
       }
@@ -756,7 +760,7 @@ __global__ __launch_bounds__(kThreads) void jpeg_huffman_kernel(const JpegDesc* 
     D.u = (int)(st >> 8) & 0xFF;
     D.k = (int)st & 0xFF;
     D.q = S[c].bpre - 1;                          // the block a mid-block start continues
-    D.pred.set(S[c].dpre[0], S[c].dpre[1], S[c].dpre[2]);
+    D.pred.set(S[c].dpre[0], S[c].dpre[1], S[c].dpre[2], S[c].dpre[3]);
     D.blk = D.k != 0 && D.q >= 0 && D.q < ch.seg_blocks ? block_ptr(d, T, coefs, ch.first_mcu, D.q)
                                                         : nullptr;
     if (ch.flags & 2) {                           // a segment's last chunk: up to its last block
@@ -815,8 +819,8 @@ __device__ void prog_segment(const JpegDesc& d, const ProgScan& S, const DHuff* 
   br.end = b1 * 8;
   br.seek(b0 * 8);
   int eobrun = 0;
-  Comp3 pred;
-  pred.set(0, 0, 0);
+  Comp4 pred;
+  pred.set(0, 0, 0, 0);
   const int p1 = 1 << S.al, m1_ = -1 * (1 << S.al);
   const bool dc = S.ss == 0, refine = S.ah != 0;
   for (int mcu = m0; mcu < m1; ++mcu) {
