@@ -862,6 +862,8 @@ def test_gemm_statout_needs_a_specialised_epilogue(L, cuda):
     (6000, 1544, 3072, 1, "bf16")])       # (all >= 128 tiles: the pp2 kernels)
 @pytest.mark.parametrize("tpw", [2, 3, 5])
 def test_gemm_tiles_per_workgroup(L, cuda, M, N, K, act, mode, tpw):
+    if not hasattr(L.lib, "vtd_diag_build"):
+        pytest.skip("the multi-tile kernel is in the diagnostic build only (VTD_LIB_PATH=libvtd_diag.so)")
     """Several output tiles per pp2 workgroup (knob VTD_KNOB_GEMM_TPW, gemm_tn_bf16_pp2_mt_kernel
     for the forward's epilogue codes; the next tile's first K-stage is loaded during the
     current tile's epilogue): every tile is computed by the same instructions, so the outputs

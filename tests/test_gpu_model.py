@@ -339,6 +339,13 @@ def test_removed_diagnostic_switches_do_not_change_logits(vtd, cuda, monkeypatch
             assert torch.equal(big(x), ref_big), (var, val)
             assert torch.equal(tiny(tx), ref_tiny), (var, val)
         monkeypatch.delenv(var)
+    # round 4: the multi-tile GEMM and the 16-query attention kernel are diagnostic-build
+    # only; their knobs leave the product library's forward unchanged
+    from vision_transformer_detector_amd import _lib as L
+    if not hasattr(L.lib, "vtd_diag_build"):
+        for knob, val in ((L.KNOB_GEMM_TPW, 2), (L.KNOB_ATTN_VARIANT, 5)):
+            with L.knob(knob, val):
+                assert torch.equal(big(x), ref_big), (knob, val)
 
 # A single-layer MLP (encoder_mlp_quantities=1) makes its one Dense both the LayerNorm-2 fold
 # consumer and the residual producer that emits the next LayerNorm's partial statistics; the

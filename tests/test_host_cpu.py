@@ -50,6 +50,8 @@ def test_removed_switches_are_not_read_by_the_library(L):
                  b"VTD_GEMM_VARIANT", b"VTD_MX_VARIANT", b"VTD_W4_SCHED", b"VTD_X4_SCHED"):
         assert name + b"\0" not in blob, name
     assert b"gemm_tn_bf16_w4" not in blob and b"gemm_mx8_x4" not in blob
+    # round 4: measured-negative / neutral kernels kept for the diagnostic build only
+    assert b"gemm_tn_bf16_pp2_mt_kernel" not in blob and b"attention_bf16_ps16_kernel" not in blob
     assert not hasattr(L.lib, "vtd_diag_build")
     # the run-time knobs are read from the environment once per process (vtd_set_knob)
     for name in (b"VTD_ATTN_VARIANT", b"VTD_ATTN_GRID", b"VTD_GEMM_NGW", b"VTD_SPLITK",

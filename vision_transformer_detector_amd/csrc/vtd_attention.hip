@@ -760,6 +760,7 @@ __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
 // V rows chunk ^ (((row >> 1) & 3) << 1) (the 8 rows x 32 B of a tr-read half-wave cover the
 // 64 banks once).  Same operations per score / output as attention_bf16_ps_kernel, summed in
 // another order: equal to within fp32 / bf16-P rounding (tested against it and fp64).
+#if VTD_DIAG   // diagnostic build only: measured neutral against attention_bf16_ps_kernel at C2
 __device__ __forceinline__ int swz_v16(int row) { return ((row >> 1) & 3) << 1; }
 __device__ __forceinline__ float xmax16(float v) {
   const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false,
@@ -985,6 +986,7 @@ int launch_bf16_ps16(const void* qkv, int B, int N, int heads, int ldqkv, float 
   VTD_LAUNCH_CHECK("attention_bf16_ps16");
   return VTD_OK;
 }
+#endif  // VTD_DIAG
 
 int launch_bf16_ps(const void* qkv, int B, int N, int heads, int ldqkv, float scale, void* out,
                    int ldo, hipStream_t stream) {
@@ -1083,9 +1085,12 @@ int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqk
     // 128-B rows and 16-B aligned row pitches), else as 2
     const bool ps_ok = dkp == 64 && N > 128 && N <= 256 && ldqkv % 8 == 0 && ldo % 8 == 0 &&
                        (int64_t)N * ldqkv * 2 < INT32_MAX && (int64_t)N * ldo * 2 < INT32_MAX;
-    // 5: the 16-query-per-wave persistent kernel at N in (192, 208] (C2), else as 4
+    // 5 (diagnostic build): the 16-query-per-wave persistent kernel at N in (192, 208] (C2),
+    // else (and in the product library) as 4
+#if VTD_DIAG
     if (v1 == 5 && ps_ok && N > 192 && N <= 208)
       return launch_bf16_ps16(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+#endif
     if ((v1 == 4 || v1 == 5) && ps_ok)
       return launch_bf16_ps(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
     if (v1 == 1) {

@@ -967,6 +967,10 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
   epilogue_generic(acc, ep, lane, M, N, m_base, n_base, e);
 }
 
+#if VTD_DIAG
+// Diagnostic build only (round 4, measured: the forward 18.9k vs 20.0k img/s with two tiles
+// per workgroup -- the next tile's K loop cannot start before the epilogue's stores are
+// acknowledged, vmcnt counting them with the prefetch; profiles/r04_tpw_trs_ab.log).
 // Several tiles per workgroup (knob VTD_KNOB_GEMM_TPW > 1, the forward's epilogue codes):
 // pp2's K loop and epilogues in a tile loop; a tile's epilogue issues the next tile's first
 // K-stage into stage 0 (the epilogue's LDS lies past it), so that the next K loop starts on
@@ -1089,6 +1093,7 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_mt_kernel(
     pre = true;
   }
 }
+#endif  // VTD_DIAG
 
 // The fp32 parity mode's 256 x 256-tile kernel: pp2's staging, ping-pong schedule and
 // epilogues with f32 operands (a 128-B K-step row = 32 f32) on v_mfma_f32_16x16x4_f32
@@ -1465,6 +1470,7 @@ template <int C>
 void pp2_launch(bool tr, dim3 g, hipStream_t stream, int M, int N, int K, const bf16_t* A, int lda,
                 const bf16_t* Bt, int ldb, int tiles_m, int tiles_n, const EpiArgs& e,
                 int ksplit = 1) {
+#if VTD_DIAG
   if constexpr (pp2_mt_code(C)) {
     if (ksplit == 1 && e.tpw > 1) {
       const dim3 gm((tiles_m * tiles_n + e.tpw - 1) / e.tpw);
@@ -1477,6 +1483,7 @@ void pp2_launch(bool tr, dim3 g, hipStream_t stream, int M, int N, int K, const 
       return;
     }
   }
+#endif
   if (tr)
     hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, true>), g, dim3(BNT), 2 * BSTAGE, stream, M,
                        N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e, ksplit);
@@ -1494,6 +1501,7 @@ void pp2_set_attributes() {
 #undef VTD_PP_FN
     for (const void* f : fns)
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
+#if VTD_DIAG
 #define VTD_MT_FN(C) reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_mt_kernel<C, false>), \
                      reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_mt_kernel<C, true>),
     const void* mts[] = {VTD_MT_FN(4 | EPI_LNF) VTD_MT_FN(5 | EPI_LNF) VTD_MT_FN(12 | EPI_STAT)
@@ -1501,6 +1509,7 @@ void pp2_set_attributes() {
 #undef VTD_MT_FN
     for (const void* f : mts)
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPP2LdsMax);
+#endif
   });
 }
 
@@ -1538,13 +1547,6 @@ void f32_pp2_launch(int M, int N, int K, const float* A, int lda, const float* B
 #undef VTD_F32_FN
     for (const void* f : fns)
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
-#define VTD_MT_FN(C) reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_mt_kernel<C, false>), \
-                     reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_mt_kernel<C, true>),
-    const void* mts[] = {VTD_MT_FN(4 | EPI_LNF) VTD_MT_FN(5 | EPI_LNF) VTD_MT_FN(12 | EPI_STAT)
-                         VTD_MT_FN(5) VTD_MT_FN(12)};
-#undef VTD_MT_FN
-    for (const void* f : mts)
-      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPP2LdsMax);
   });
   EpiArgs e = make_epi_args(epi);
   e.ngw = tile_group_width(tiles_n);
@@ -1630,7 +1632,7 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
     pp2_set_attributes();
     EpiArgs e = make_epi_args(epi);
     e.ngw = ngw;
-    e.tpw = pp2_tpw();
+    e.tpw = VTD_DIAG ? pp2_tpw() : 1;   // several tiles per workgroup: diagnostic build only
     const int code = pp2_code(epi);
     // transposed accumulators + register-direct epilogue for activation layers (mlp1 -5 %,
     // mlp2 -1.5 %), LDS-staged row vectors for the others (attn_out -10 %, mlp3 -4 %);
