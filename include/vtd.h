@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define VTD_ABI_VERSION 13
+#define VTD_ABI_VERSION 14
 #define VTD_KALIGN 64          /* K / row padding granule, elements              */
 #define VTD_MAX_MLP 16         /* max encoder_mlp_quantities                     */
 #define VTD_MAX_HEAD 64        /* max mlp_head layers * repeats                   */
@@ -321,6 +321,21 @@ int vtd_jpeg_decode(const uint8_t* const* jpegs, const size_t* lens, int n, uint
                     const int64_t* out_offsets, void* workspace_dev, size_t workspace_bytes,
                     void* stream);
 
+/* PNG decode, tf.image.decode_image(file, channels=3) for PNG (vision_transformer_utilities.py
+ * :431) as TF's libpng path does it: every colour type and bit depth (1-16), Adam7
+ * interlacing; palette -> RGB, gray -> RGB, alpha / tRNS dropped, 16-bit -> high byte.  The
+ * chunk walk (critical-chunk CRCs checked) and the zlib inflate run on the host over a few
+ * threads; the filtered scanlines are copied to the workspace on `stream` (pinned staging the
+ * library reuses) and un-filtered + converted on the device, image i written as RGB uint8 HWC
+ * at out_dev + out_offsets[i].  Same calling convention as the JPEG entry points;
+ * vtd_png_info's comps = samples per pixel of the file (1-4). */
+int vtd_png_info(const uint8_t* png, size_t len, int* h, int* w, int* comps);
+int vtd_png_workspace_bytes(const uint8_t* const* pngs, const size_t* lens, int n,
+                            int32_t* dims, size_t* bytes);
+int vtd_png_decode(const uint8_t* const* pngs, const size_t* lens, int n, uint8_t* out_dev,
+                   const int64_t* out_offsets, void* workspace_dev, size_t workspace_bytes,
+                   void* stream);
+
 /* ---------------------------------------------------------------- forward ------ */
 /* model(images, training=False) (vtd.py:579-581, ipynb:836):
  * images NHWC fp32 [B][H][W][C] in [-1, 1] -> logits fp32 [B][17][6] (pre-sigmoid),
@@ -378,7 +393,8 @@ int vtd_profile_read(double* ms, int64_t* launches, double* flops, int n_classes
  *     1 = the register-staged first kernel.
  *   VTD_KNOB_ATTN_GRID (VTD_ATTN_GRID): persistent attention workgroups (default: CUs).
  *   VTD_KNOB_GEMM_NGW (VTD_GEMM_NGW): GEMM tile-order group width (0 = row-major).
- *   VTD_KNOB_SPLITK (VTD_SPLITK): 0 disables the head's split-K (changes workspace size).
+ *   VTD_KNOB_SPLITK (VTD_SPLITK): 0 disables the head's split-K, a value >= 64 sets its
+ *     workgroup target per launch (default 256); both change the workspace size.
  *   VTD_KNOB_JPEG_CHUNK_BITS (VTD_JPEG_CHUNK_BITS): Huffman chunk length of vtd_jpeg_decode.
  *   VTD_KNOB_SKINNY (VTD_SKINNY): 0 keeps the head's narrow bf16 layers (N <= 320) on the
  *     128 x 128 kernel instead of the skinny one.

@@ -1,0 +1,76 @@
+"""PNG host side (vtd_png_info / vtd_png_workspace_bytes; no GPU): header walk over every
+colour type / bit depth Pillow writes, Adam7, and the refusals libpng makes (bad signature,
+critical-chunk CRC, truncation, palette without PLTE)."""
+import ctypes
+import io
+import struct
+import zlib
+
+import numpy as np
+import pytest
+from PIL import Image
+
+
+@pytest.fixture(scope="module")
+def L():
+    from vision_transformer_detector_amd import _lib
+    return _lib
+
+
+def _png(arr, mode, **kw):
+    b = io.BytesIO()
+    Image.fromarray(arr, mode=mode).save(b, format="PNG", **kw)
+    return b.getvalue()
+
+
+def _info(L, f):
+    h, w, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    rc = L.lib.vtd_png_info(f, len(f), ctypes.byref(h), ctypes.byref(w), ctypes.byref(c))
+    return rc, (h.value, w.value, c.value)
+
+
+def _ws(L, files):
+    n = len(files)
+    ptrs = (ctypes.c_char_p * n)(*files)
+    lens = (ctypes.c_size_t * n)(*[len(f) for f in files])
+    dims = np.zeros((n, 2), np.int32)
+    b = ctypes.c_size_t()
+    rc = L.lib.vtd_png_workspace_bytes(ptrs, lens, n, dims.ctypes.data, ctypes.byref(b))
+    return rc, dims, b.value
+
+
+def _chunk(t, body):
+    return struct.pack(">I", len(body)) + t + body + struct.pack(">I", zlib.crc32(t + body))
+
+
+def test_png_header_walk(L):
+    rng = np.random.default_rng(0)
+    rgb = rng.integers(0, 256, (9, 13, 3), dtype=np.uint8)
+    cases = [(_png(rgb, "RGB"), 3), (_png(rgb[..., 0], "L"), 1),
+             (_png(np.dstack([rgb, rgb[..., :1]]), "RGBA"), 4),
+             (_png(rgb, "RGB", optimize=True), 3),
+             (_png((rgb[..., 0] > 127), "1"), 1)]
+    pal = Image.fromarray(rgb).convert("P", palette=Image.ADAPTIVE, colors=16)
+    b = io.BytesIO()
+    pal.save(b, format="PNG")
+    cases.append((b.getvalue(), 1))
+    for f, comps in cases:
+        rc, dims = _info(L, f)
+        assert rc == 0 and dims == (9, 13, comps), (dims, L.lib.vtd_last_error())
+    rc, dims, ws = _ws(L, [c[0] for c in cases])
+    assert rc == 0 and ws > 0 and (dims == [9, 13]).all()
+
+
+def test_png_refusals_name_the_reason(L):
+    f = _png(np.zeros((4, 5, 3), np.uint8), "RGB")
+    assert _info(L, b"GIF89a" + f[6:])[0] != 0 and b"not a PNG" in L.lib.vtd_last_error()
+    i = f.index(b"IHDR")
+    bad = f[:i + 5] + bytes([f[i + 5] ^ 1]) + f[i + 6:]          # IHDR body changed, CRC not
+    assert _info(L, bad)[0] != 0 and b"CRC" in L.lib.vtd_last_error()
+    assert _info(L, f[:-12])[0] != 0 and b"IEND" in L.lib.vtd_last_error()
+    sig = b"\x89PNG\r\n\x1a\n"
+    ihdr = _chunk(b"IHDR", struct.pack(">IIBBBBB", 4, 4, 8, 3, 0, 0, 0))
+    nopal = sig + ihdr + _chunk(b"IDAT", zlib.compress(bytes(4 * 5))) + _chunk(b"IEND", b"")
+    assert _info(L, nopal)[0] != 0 and b"PLTE" in L.lib.vtd_last_error()
+    rc, _, _ = _ws(L, [f, nopal])
+    assert rc != 0 and b"image 1" in L.lib.vtd_last_error()

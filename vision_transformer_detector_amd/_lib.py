@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must precede loading libvtd.so, see module doc)
 LIB_PATH = os.environ.get("VTD_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                           "libvtd.so")
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 KALIGN = 64
 MAX_MLP = 16
 MAX_HEAD = 64
@@ -128,6 +128,12 @@ SIGNATURES = {
                                          ctypes.POINTER(c_size_t)]),
     "vtd_jpeg_decode": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                                 c_size_t, c_void_p]),
+    "vtd_png_info": (c_int, [c_void_p, c_size_t, ctypes.POINTER(c_int), ctypes.POINTER(c_int),
+                             ctypes.POINTER(c_int)]),
+    "vtd_png_workspace_bytes": (c_int, [c_void_p, c_void_p, c_int, c_void_p,
+                                        ctypes.POINTER(c_size_t)]),
+    "vtd_png_decode": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                               c_size_t, c_void_p]),
     "vtd_iou": (c_int, [c_void_p, c_void_p, c_int64, c_int, c_void_p, c_void_p]),
     "vtd_map_reset": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     "vtd_map_update": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,

@@ -1735,9 +1735,12 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
 // so its operand traffic stays well above its 256 KiB fp32 partial tile; 1 = no split.
 // Fixed targets (not the device's CU count) so that workspace sizing needs no device.
 // VTD_SPLITK=0 / knob VTD_KNOB_SPLITK = 0 disables it.
-constexpr int kSplitTarget = 256, kSplitMinSteps = 8;
+constexpr int kSplitTargetDefault = 256, kSplitMinSteps = 8;
 int gemm_splitk_choice(int M, int N, int K, int dtype) {
-  if (knob(VTD_KNOB_SPLITK) == 0) return 1;
+  const int ks = knob(VTD_KNOB_SPLITK);
+  if (ks == 0) return 1;
+  // knob value >= 64: the workgroup target itself (A/B of the concurrent micro-batch halves)
+  const int kSplitTarget = ks >= 64 ? ks : kSplitTargetDefault;
   if (dtype != VTD_BF16 || N <= 64 || K % 64 != 0 || M <= 0) return 1;
   const int tiles = ((M + BBM - 1) / BBM) * ((N + BBN - 1) / BBN);
   const int nk = K / 64;

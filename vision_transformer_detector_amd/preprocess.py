@@ -102,6 +102,69 @@ def decode_jpegs(files, device="cuda", stream=None):
     return pixels, offsets, sizes
 
 
+def _decode_with(kind, files, pixels, offsets, dev, stream):
+    """Run the `kind` ("jpeg" / "png") device decoder on `files` into `pixels` at `offsets`."""
+    import ctypes
+    n = len(files)
+    ptrs = (ctypes.c_char_p * n)(*files)
+    lens = (ctypes.c_size_t * n)(*[len(f) for f in files])
+    dims = np.zeros((n, 2), np.int32)
+    ws_bytes = ctypes.c_size_t()
+    rc = getattr(L.lib, f"vtd_{kind}_workspace_bytes")(ptrs, lens, n, dims.ctypes.data,
+                                                      ctypes.byref(ws_bytes))
+    if rc != 0:
+        raise ValueError(L.lib.vtd_last_error().decode())
+    ws = torch.empty(max(1, int(ws_bytes.value)), dtype=torch.uint8, device=dev)
+    offs = (ctypes.c_int64 * n)(*[int(o) for o in offsets])
+    _on_stream(stream, dev, pixels, ws)
+    with torch.cuda.device(dev):
+        L.check(getattr(L.lib, f"vtd_{kind}_decode")(ptrs, lens, n, L.ptr(pixels), offs, L.ptr(ws),
+                                                    ws_bytes.value, L.stream_ptr(stream)),
+                f"{kind}_decode")
+
+
+def _kind(f: bytes) -> str:
+    if f[:3] == b"\xff\xd8\xff":
+        return "jpeg"
+    if f[:8] == b"\x89PNG\r\n\x1a\n":
+        return "png"
+    raise ValueError("decode_images: not a JPEG or PNG file (GIF / BMP are not supported)")
+
+
+def decode_images(files, device="cuda", stream=None):
+    """`tf.image.decode_image(f, channels=3)` (vision_transformer_utilities.py:431) for a batch
+    of JPEG and PNG files (by their signature), decoded on the device (vtd_jpeg_decode /
+    vtd_png_decode) into one packed RGB uint8 buffer -> (pixels, per-image byte offsets,
+    [(height, width), ...]) as `decode_jpegs`."""
+    import ctypes
+    if len(files) == 0:
+        raise ValueError("decode_images: empty file list")
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise ValueError(f"decode_images runs on a HIP device, got {dev}")
+    files = [bytes(f) for f in files]
+    kinds = [_kind(f) for f in files]
+    sizes = []
+    for f, k in zip(files, kinds):
+        h, w, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        rc = getattr(L.lib, f"vtd_{k}_info")(f, len(f), ctypes.byref(h), ctypes.byref(w),
+                                            ctypes.byref(c))
+        if rc != 0:
+            raise ValueError(L.lib.vtd_last_error().decode())
+        sizes.append((h.value, w.value))
+    n = len(files)
+    offsets = np.zeros(n, np.int64)
+    offsets[1:] = np.cumsum([h * w * 3 for h, w in sizes])[:-1]
+    total = int(offsets[-1]) + sizes[-1][0] * sizes[-1][1] * 3
+    pixels = torch.empty(total, dtype=torch.uint8, device=dev)
+    for kind in ("jpeg", "png"):
+        idx = [i for i in range(n) if kinds[i] == kind]
+        if idx:
+            _decode_with(kind, [files[i] for i in idx], pixels, [offsets[i] for i in idx], dev,
+                         stream)
+    return pixels, offsets, sizes
+
+
 def _on_stream(stream, dev, *tensors):
     """Before launching on a caller-given `stream` that is not the current one: order it after
     the current stream's work (the allocations and host-to-device copies of the inputs were
@@ -119,8 +182,8 @@ def _on_stream(stream, dev, *tensors):
 def get_image_tensors_from_files(paths_or_bytes, target_height: int = MODEL_IMAGE_HEIGHT,
                                  target_width: int = MODEL_IMAGE_WIDTH, device="cuda",
                                  stream=None):
-    """`_get_image_tensor_coco` for a batch of JPEG files (paths or bytes): read, decode on
-    the device (decode_jpegs), resize_with_pad / clip / normalise on the device ->
+    """`_get_image_tensor_coco` for a batch of JPEG / PNG files (paths or bytes): read, decode
+    on the device (decode_images), resize_with_pad / clip / normalise on the device ->
     (images (B, target_height, target_width, 3) fp32 in [-1, 1], original sizes)."""
     files = []
     for p in paths_or_bytes:
@@ -129,7 +192,7 @@ def get_image_tensors_from_files(paths_or_bytes, target_height: int = MODEL_IMAG
         else:
             with open(p, "rb") as f:
                 files.append(f.read())
-    pixels, offsets, sizes = decode_jpegs(files, device=device, stream=stream)
+    pixels, offsets, sizes = decode_images(files, device=device, stream=stream)
     dev = torch.device(device)
     for h, w in sizes:
         if not _resized_side_positive(h, w, target_height, target_width):
