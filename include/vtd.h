@@ -336,6 +336,17 @@ int vtd_png_decode(const uint8_t* const* pngs, const size_t* lens, int n, uint8_
                    const int64_t* out_offsets, void* workspace_dev, size_t workspace_bytes,
                    void* stream);
 
+/* BMP decode, tf.image.decode_image(file, channels=3) for BMP as TF's decode_bmp does it:
+ * 24-bit uncompressed rows (bottom-up, or top-down for a negative height), BGR -> RGB; other
+ * bit depths are refused as TF refuses a bits-per-pixel / channels mismatch.  Same calling
+ * convention as the PNG / JPEG entry points. */
+int vtd_bmp_info(const uint8_t* bmp, size_t len, int* h, int* w, int* comps);
+int vtd_bmp_workspace_bytes(const uint8_t* const* bmps, const size_t* lens, int n,
+                            int32_t* dims, size_t* bytes);
+int vtd_bmp_decode(const uint8_t* const* bmps, const size_t* lens, int n, uint8_t* out_dev,
+                   const int64_t* out_offsets, void* workspace_dev, size_t workspace_bytes,
+                   void* stream);
+
 /* ---------------------------------------------------------------- forward ------ */
 /* model(images, training=False) (vtd.py:579-581, ipynb:836):
  * images NHWC fp32 [B][H][W][C] in [-1, 1] -> logits fp32 [B][17][6] (pre-sigmoid),

@@ -178,3 +178,30 @@ def test_png_corrupt_stream_raises(cuda):
     bad = f[:i - 4] + _chunk(b"IDAT", body) + f[i + 8 + ln:]
     with pytest.raises((ValueError, RuntimeError), match="zlib|truncated"):
         decode_images([bad], device=cuda)
+
+
+def test_bmp_decode_bottom_up_and_top_down(cuda):
+    """24-bit BMP (TF decode_bmp): bottom-up rows from Pillow's encoder and the same file made
+    top-down (negative height, rows reversed), widths with 4-byte row padding."""
+    from vision_transformer_detector_amd.preprocess import decode_images
+    files, refs = [], []
+    for k, (h, w) in enumerate([(7, 11), (16, 16), (1, 1), (33, 50)]):
+        rgb = np.random.default_rng(k).integers(0, 256, (h, w, 3), dtype=np.uint8)
+        b = io.BytesIO()
+        Image.fromarray(rgb).save(b, format="BMP")
+        f = b.getvalue()
+        files.append(f)
+        refs.append(rgb)
+        off = int.from_bytes(f[10:14], "little")
+        row = (24 * w + 31) // 32 * 4
+        rows = [f[off + r * row:off + (r + 1) * row] for r in range(h)]
+        td = bytearray(f[:off] + b"".join(rows[::-1]))
+        td[22:26] = (-h).to_bytes(4, "little", signed=True)
+        files.append(bytes(td))
+        refs.append(rgb)
+    pixels, offsets, sizes = decode_images(files, device=cuda)
+    torch.cuda.synchronize()
+    got = pixels.cpu().numpy()
+    for i, ref in enumerate(refs):
+        h, w = sizes[i]
+        assert np.array_equal(got[offsets[i]:offsets[i] + h * w * 3].reshape(h, w, 3), ref), i

@@ -74,3 +74,24 @@ def test_png_refusals_name_the_reason(L):
     assert _info(L, nopal)[0] != 0 and b"PLTE" in L.lib.vtd_last_error()
     rc, _, _ = _ws(L, [f, nopal])
     assert rc != 0 and b"image 1" in L.lib.vtd_last_error()
+
+
+def test_bmp_header_and_refusals(L):
+    """BMP (TF decode_bmp): 24-bit files pass; 32-bit and 8-bit are refused as TF refuses a
+    bits-per-pixel / channels mismatch for channels = 3."""
+    rng = np.random.default_rng(1)
+    rgb = rng.integers(0, 256, (7, 11, 3), dtype=np.uint8)
+    b = io.BytesIO()
+    Image.fromarray(rgb).save(b, format="BMP")
+    f = b.getvalue()
+    h, w, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    assert L.lib.vtd_bmp_info(f, len(f), ctypes.byref(h), ctypes.byref(w), ctypes.byref(c)) == 0
+    assert (h.value, w.value, c.value) == (7, 11, 3)
+    for mode in ("RGBA", "L"):
+        b = io.BytesIO()
+        Image.fromarray(rgb).convert(mode).save(b, format="BMP")
+        g = b.getvalue()
+        assert L.lib.vtd_bmp_info(g, len(g), ctypes.byref(h), ctypes.byref(w), ctypes.byref(c)) != 0
+        assert b"bits-per-pixel" in L.lib.vtd_last_error()
+    assert L.lib.vtd_bmp_info(f[:60], 60, ctypes.byref(h), ctypes.byref(w), ctypes.byref(c)) != 0
+    assert b"truncated" in L.lib.vtd_last_error()

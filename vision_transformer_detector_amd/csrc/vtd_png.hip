@@ -376,3 +376,162 @@ extern "C" int vtd_png_decode(const uint8_t* const* pngs, const size_t* lens, in
   VTD_LAUNCH_CHECK("png_unfilter");
   return VTD_OK;
 }
+
+// ------------------------------------------------------------------ BMP
+// `tf.image.decode_image(file, channels=3)` on BMP files goes through TF's decode_bmp
+// (tensorflow/core/kernels/image/decode_bmp_op.cc): uncompressed rows, bottom-up unless the
+// height is negative, each row padded to 4 bytes, BGR(A) -> RGB(A), and the file's
+// bits-per-pixel / 8 must equal the requested channel count -- so with channels = 3 only
+// 24-bit files decode; the others are refused by name here as TF refuses them.  The host
+// reads the 54-byte header; the pixel array goes to the workspace in one copy and
+// bmp_convert_kernel (one thread per output pixel) writes the RGB8 rows.
+namespace vtd {
+namespace {
+
+struct BmpDesc {
+  int w, h, top_down, row_size;
+  int64_t data_off, out_off;
+};
+
+__global__ __launch_bounds__(256) void bmp_convert_kernel(const BmpDesc* __restrict__ descs,
+                                                          const uint8_t* __restrict__ data,
+                                                          uint8_t* __restrict__ out) {
+  const BmpDesc& d = descs[blockIdx.y];
+  const int64_t npx = (int64_t)d.w * d.h;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < npx; i += (int64_t)gridDim.x * 256) {
+    const int y = (int)(i / d.w), x = (int)(i - (int64_t)y * d.w);
+    const int sy = d.top_down ? y : d.h - 1 - y;
+    const uint8_t* s = data + d.data_off + (int64_t)sy * d.row_size + 3 * x;
+    uint8_t* o = out + d.out_off + 3 * i;
+    o[0] = s[2];
+    o[1] = s[1];
+    o[2] = s[0];
+  }
+}
+
+int32_t le32(const uint8_t* p) { return (int32_t)((uint32_t)p[0] | p[1] << 8 | p[2] << 16 | (uint32_t)p[3] << 24); }
+int le16(const uint8_t* p) { return p[0] | p[1] << 8; }
+
+bool parse_bmp(const uint8_t* b, size_t n, BmpDesc& d, int64_t& pix_off, std::string& err) {
+  memset(&d, 0, sizeof(d));
+  if (n < 54 || b[0] != 'B' || b[1] != 'M') { err = "bmp: not a BMP file"; return false; }
+  pix_off = le32(b + 10);
+  const int32_t w = le32(b + 18), h = le32(b + 22);
+  const int bpp = le16(b + 28);
+  const int32_t comp = le32(b + 30);
+  if (comp != 0) { err = "bmp: compressed BMP files are not supported (TF decode_bmp reads BI_RGB rows)"; return false; }
+  if (bpp != 24) {
+    err = "bmp: " + std::to_string(bpp) + "-bit file: TF's decode_bmp needs bits-per-pixel / 8 == "
+          "the 3 requested channels";
+    return false;
+  }
+  if (w <= 0 || h == 0 || h == INT32_MIN) { err = "bmp: bad size"; return false; }
+  d.w = w;
+  d.h = h < 0 ? -h : h;
+  d.top_down = h < 0;
+  d.row_size = (int)(((int64_t)24 * w + 31) / 32 * 4);
+  if (pix_off < 54 || (uint64_t)pix_off + (uint64_t)d.row_size * d.h > n) {
+    err = "bmp: truncated pixel array";
+    return false;
+  }
+  return true;
+}
+
+int bmp_plan(const uint8_t* const* files, const size_t* lens, int n, std::vector<BmpDesc>& D,
+             std::vector<int64_t>& pix, int32_t* dims, size_t& data_off, size_t& total) {
+  VTD_CHECK_ARG(files && lens && n > 0, "bmp: bad arguments");
+  D.resize(n);
+  pix.resize(n);
+  size_t data = 0;
+  for (int i = 0; i < n; ++i) {
+    VTD_CHECK_ARG(files[i] && lens[i] > 0, "bmp: null / empty image");
+    std::string err;
+    if (!parse_bmp(files[i], lens[i], D[i], pix[i], err))
+      return fail(VTD_ERR_UNSUPPORTED, err + " (image " + std::to_string(i) + ")");
+    D[i].data_off = (int64_t)data;
+    data += align256((size_t)D[i].row_size * D[i].h);
+    if (dims) {
+      dims[2 * i] = D[i].h;
+      dims[2 * i + 1] = D[i].w;
+    }
+  }
+  data_off = align256((size_t)n * sizeof(BmpDesc));
+  total = data_off + data;
+  return VTD_OK;
+}
+
+}  // namespace
+}  // namespace vtd
+
+extern "C" int vtd_bmp_info(const uint8_t* bmp, size_t len, int* h, int* w, int* comps) {
+  VTD_CHECK_ARG(bmp && len > 0 && h && w && comps, "bmp_info: bad arguments");
+  vtd::BmpDesc d;
+  int64_t pix = 0;
+  std::string err;
+  if (!vtd::parse_bmp(bmp, len, d, pix, err)) return vtd::fail(VTD_ERR_UNSUPPORTED, err);
+  *h = d.h;
+  *w = d.w;
+  *comps = 3;
+  return VTD_OK;
+}
+
+extern "C" int vtd_bmp_workspace_bytes(const uint8_t* const* bmps, const size_t* lens, int n,
+                                       int32_t* dims, size_t* bytes) {
+  VTD_CHECK_ARG(bytes, "bmp_workspace_bytes: null bytes pointer");
+  std::vector<vtd::BmpDesc> D;
+  std::vector<int64_t> pix;
+  size_t data_off = 0, total = 0;
+  const int rc = vtd::bmp_plan(bmps, lens, n, D, pix, dims, data_off, total);
+  if (rc != VTD_OK) return rc;
+  *bytes = total;
+  return VTD_OK;
+}
+
+extern "C" int vtd_bmp_decode(const uint8_t* const* bmps, const size_t* lens, int n,
+                              uint8_t* out_dev, const int64_t* out_offsets, void* workspace_dev,
+                              size_t workspace_bytes, void* stream) {
+  using namespace vtd;
+  VTD_CHECK_ARG(out_dev && out_offsets && workspace_dev, "bmp_decode: null pointer");
+  VTD_CHECK_ARG(n <= 65535, "bmp_decode: at most 65535 images per call");
+  std::vector<BmpDesc> D;
+  std::vector<int64_t> pix;
+  size_t data_off = 0, total = 0;
+  int rc = bmp_plan(bmps, lens, n, D, pix, nullptr, data_off, total);
+  if (rc != VTD_OK) return rc;
+  if (workspace_bytes < total) return fail(VTD_ERR_WORKSPACE, "bmp_decode: workspace too small");
+  int64_t maxpx = 0;
+  for (int i = 0; i < n; ++i) {
+    D[i].out_off = out_offsets[i];
+    maxpx = std::max<int64_t>(maxpx, (int64_t)D[i].w * D[i].h);
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  PngStaging& sg = png_staging();
+  std::lock_guard<std::mutex> g(sg.mu);
+  if (sg.done) {
+    const hipError_t e = hipEventSynchronize(sg.done);
+    if (e != hipSuccess) return fail(VTD_ERR_HIP, std::string("bmp: ") + hipGetErrorString(e));
+  } else if (hipEventCreateWithFlags(&sg.done, hipEventDisableTiming) != hipSuccess) {
+    return fail(VTD_ERR_HIP, "bmp: event create failed");
+  }
+  if (sg.cap < total) {
+    if (sg.host) (void)hipHostFree(sg.host);
+    sg.host = nullptr;
+    sg.cap = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&sg.host), total) != hipSuccess)
+      return fail(VTD_ERR_HIP, "bmp: pinned staging allocation failed");
+    sg.cap = total;
+  }
+  memcpy(sg.host, D.data(), n * sizeof(BmpDesc));
+  for (int i = 0; i < n; ++i)
+    memcpy(sg.host + data_off + D[i].data_off, bmps[i] + pix[i], (size_t)D[i].row_size * D[i].h);
+  uint8_t* ws = static_cast<uint8_t*>(workspace_dev);
+  hipError_t e = hipMemcpyAsync(ws, sg.host, total, hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipEventRecord(sg.done, st);
+  if (e != hipSuccess) return fail(VTD_ERR_HIP, std::string("bmp: ") + hipGetErrorString(e));
+  ProfScope ps(st, PROF_OTHER, 0.0);
+  const unsigned gx = (unsigned)std::min<int64_t>(1024, (maxpx + 255) / 256);
+  hipLaunchKernelGGL(bmp_convert_kernel, dim3(gx, n), dim3(256), 0, st,
+                     reinterpret_cast<const BmpDesc*>(ws), ws + data_off, out_dev);
+  VTD_LAUNCH_CHECK("bmp_convert");
+  return VTD_OK;
+}

@@ -128,13 +128,15 @@ def _kind(f: bytes) -> str:
         return "jpeg"
     if f[:8] == b"\x89PNG\r\n\x1a\n":
         return "png"
-    raise ValueError("decode_images: not a JPEG or PNG file (GIF / BMP are not supported)")
+    if f[:2] == b"BM":
+        return "bmp"
+    raise ValueError("decode_images: not a JPEG, PNG or BMP file (GIF is not supported)")
 
 
 def decode_images(files, device="cuda", stream=None):
     """`tf.image.decode_image(f, channels=3)` (vision_transformer_utilities.py:431) for a batch
-    of JPEG and PNG files (by their signature), decoded on the device (vtd_jpeg_decode /
-    vtd_png_decode) into one packed RGB uint8 buffer -> (pixels, per-image byte offsets,
+    of JPEG, PNG and BMP files (by their signature), decoded on the device (vtd_jpeg_decode /
+    vtd_png_decode / vtd_bmp_decode) into one packed RGB uint8 buffer -> (pixels, per-image byte offsets,
     [(height, width), ...]) as `decode_jpegs`."""
     import ctypes
     if len(files) == 0:
@@ -157,7 +159,7 @@ def decode_images(files, device="cuda", stream=None):
     offsets[1:] = np.cumsum([h * w * 3 for h, w in sizes])[:-1]
     total = int(offsets[-1]) + sizes[-1][0] * sizes[-1][1] * 3
     pixels = torch.empty(total, dtype=torch.uint8, device=dev)
-    for kind in ("jpeg", "png"):
+    for kind in ("jpeg", "png", "bmp"):
         idx = [i for i in range(n) if kinds[i] == kind]
         if idx:
             _decode_with(kind, [files[i] for i in idx], pixels, [offsets[i] for i in idx], dev,
