@@ -634,7 +634,9 @@ __device__ __forceinline__ void pp2_issue(char* smem, const PP2BufSrc& src, int 
 // pre: K-tile 0 was issued by the caller (pp2_prefetch, during the previous output tile's
 // epilogue, whose LDS staging lies past stage 0): wait until every wave has left that epilogue
 // before K-tile 1 is loaded over it.
-template <bool TR, bool F32 = false>
+// NB (diagnostic build, VTD_PP2_DG & 32, wrong outputs): the K loop's per-phase barriers
+// dropped -- the cost of the ping-pong synchronisation itself
+template <bool TR, bool F32 = false, bool NB = false>
 __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, const PP2BufSrc& src,
                                              int nk, int wave, int wm, int wn, int fr, int fg,
                                              uint64_t* t_prologue = nullptr, bool pre = false) {
@@ -672,26 +674,26 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
     if constexpr (n1) pp2_issue<1>(smem, src, wave, kt + 1, (kt + 1) & 1);
     if constexpr (n1) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    pp_barrier();
+    if constexpr (!NB) pp_barrier();
     if constexpr (TR) pp_mfma_t<0, 0, F32>(acc, a, b0);
     else pp_mfma<0, 0, F32>(acc, a, b0);
-    pp_barrier();
+    if constexpr (!NB) pp_barrier();
     // ---- P1
     if constexpr (TR) pp_load_b_t(b1, st + 3 * 16384, rb, fr, fg);
     else pp_load_b(b1, st + 3 * 16384, rb, fr, fg);
     if constexpr (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    pp_barrier();
+    if constexpr (!NB) pp_barrier();
     if constexpr (TR) pp_mfma_t<0, 2, F32>(acc, a, b1);
     else pp_mfma<0, 2, F32>(acc, a, b1);
-    pp_barrier();
+    if constexpr (!NB) pp_barrier();
     // ---- P2
     pp_load_a(a, st + 1 * 16384, ra, fr, fg);
     if constexpr (n2) pp2_issue<0>(smem, src, wave, kt + 2, kt & 1);
-    pp_barrier();
+    if constexpr (!NB) pp_barrier();
     if constexpr (TR) pp_mfma_t<4, 2, F32>(acc, a, b1);
     else pp_mfma<4, 2, F32>(acc, a, b1);
-    pp_barrier();
+    if constexpr (!NB) pp_barrier();
     // ---- P3
     if constexpr (n2) {
       pp2_issue<2>(smem, src, wave, kt + 2, kt & 1);
@@ -700,10 +702,10 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    pp_barrier();
+    if constexpr (!NB) pp_barrier();
     if constexpr (TR) pp_mfma_t<4, 0, F32>(acc, a, b0);
     else pp_mfma<4, 0, F32>(acc, a, b0);
-    pp_barrier();
+    if constexpr (!NB) pp_barrier();
   };
   int kt = 0;
   for (; kt + 2 < nk; ++kt) step(kt, std::true_type{}, std::true_type{});
@@ -900,7 +902,8 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
     ts[0] = __builtin_amdgcn_s_memtime();
     rt0 = __builtin_amdgcn_s_memrealtime();
   }
-  pp2_mainloop<TR>(acc, smem, src, nk, wave, wm, wn, fr, fg, (DG & 16) ? &ts[1] : nullptr);
+  pp2_mainloop<TR, false, (DG & 32) != 0>(acc, smem, src, nk, wave, wm, wn, fr, fg,
+                                           (DG & 16) ? &ts[1] : nullptr);
   if constexpr ((DG & 16) != 0) ts[2] = __builtin_amdgcn_s_memtime();
   const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
 #if VTD_DIAG
@@ -1660,7 +1663,9 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
                                 reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, false, 8>),
                                 reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, true, 8>),
                                 reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, false, 16>),
-                                reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, true, 16>)})
+                                reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, true, 16>),
+                                reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, false, 32>),
+                                reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_kernel<C, true, 32>)})
             (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
         });
 #define VTD_DG_L(D)                                                                                \
@@ -1670,7 +1675,7 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
     else hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, false, D>), g, dim3(BNT), lds,             \
                             stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e, 1);          \
   }
-        VTD_DG_L(1) VTD_DG_L(2) VTD_DG_L(4) VTD_DG_L(8) VTD_DG_L(16)
+        VTD_DG_L(1) VTD_DG_L(2) VTD_DG_L(4) VTD_DG_L(8) VTD_DG_L(16) VTD_DG_L(32)
 #undef VTD_DG_L
       };
       switch (code) {
