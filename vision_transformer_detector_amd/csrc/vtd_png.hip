@@ -185,6 +185,10 @@ bool parse_png(const uint8_t* b, size_t n, PngDesc& d, std::vector<std::pair<siz
       d.depth = body[8];
       d.ctype = body[9];
       d.interlace = body[12];
+      if ((int64_t)be32(body) * be32(body + 4) > ((int64_t)1 << 28)) {
+        err = "png: image larger than 2^28 pixels";
+        return false;
+      }
       if (d.w <= 0 || d.h <= 0 || body[10] != 0 || body[11] != 0 || d.interlace > 1) {
         err = "png: bad IHDR (size, compression, filter or interlace method)";
         return false;
@@ -426,6 +430,10 @@ bool parse_bmp(const uint8_t* b, size_t n, BmpDesc& d, int64_t& pix_off, std::st
     return false;
   }
   if (w <= 0 || h == 0 || h == INT32_MIN) { err = "bmp: bad size"; return false; }
+  if ((int64_t)w * (h < 0 ? -(int64_t)h : h) > ((int64_t)1 << 28)) {
+    err = "bmp: image larger than 2^28 pixels";
+    return false;
+  }
   d.w = w;
   d.h = h < 0 ? -h : h;
   d.top_down = h < 0;
