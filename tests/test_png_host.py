@@ -95,3 +95,17 @@ def test_bmp_header_and_refusals(L):
         assert b"bits-per-pixel" in L.lib.vtd_last_error()
     assert L.lib.vtd_bmp_info(f[:60], 60, ctypes.byref(h), ctypes.byref(w), ctypes.byref(c)) != 0
     assert b"truncated" in L.lib.vtd_last_error()
+
+
+def test_decode_images_routes_by_signature():
+    """decode_images picks the decoder by file signature (no GPU needed for the routing)."""
+    from vision_transformer_detector_amd.preprocess import _kind
+    rgb = np.zeros((4, 4, 3), np.uint8)
+    for fmt, kind in (("JPEG", "jpeg"), ("PNG", "png"), ("BMP", "bmp")):
+        b = io.BytesIO()
+        Image.fromarray(rgb).save(b, format=fmt)
+        assert _kind(b.getvalue()) == kind
+    b = io.BytesIO()
+    Image.fromarray(rgb).save(b, format="GIF")
+    with pytest.raises(ValueError, match="GIF"):
+        _kind(b.getvalue())
