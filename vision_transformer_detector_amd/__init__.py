@@ -6,6 +6,13 @@ kwargs, NHWC fp32 images in, (B, 17, 6) logits out, `transform_predictions` deco
 All arithmetic runs in hand-written gfx950 HIP kernels in `libvtd.so` (C-ABI:
 `include/vtd.h`); importing this package fails if that library is missing.
 """
+import os as _os
+
+# Kernel arguments in device memory (HIP runtime option; +1.8 % on the C2 forward,
+# profiles/r04_dev_kernarg_ab.log).  Takes effect only if the HIP runtime has not been
+# initialised yet in this process; an explicit setting by the caller wins.
+_os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
 from .detector import (Constants, Model, create_vision_transformer_detector,  # noqa: F401
                        decode_detections, detection_list, keras_default_init,
                        keras_weight_names, transform_predictions)
