@@ -12,7 +12,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -s --timeout 300 --time
 tail -1 $O/gpu_tests.log
 timeout -k 10 300 python bench.py > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
 tail -1 $O/bench.log | cut -c1-300
-P=$R/vision_transformer_detector_amd/libvtd_prev.so   # (A/B only when present)
+P=$R/vision_transformer_detector_amd/libvtd_prev.so
 if [ -f $P ]; then
   for r in 1 2; do
     VTD_LIB_PATH=$P timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 > $O/ab_prev_$r.log 2>&1 || { tail -5 $O/ab_prev_$r.log; exit 1; }
