@@ -874,11 +874,12 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int v = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int split = v / nt, tile = v - split * nt;
+  // one K range (the forward's launches): no division by the tile count or split count
+  const int split = ksplit > 1 ? v / nt : 0, tile = v - split * nt;
   int tm, tn;
-  tile_coords(tile, tiles_m, tiles_n, e.ngw, tm, tn);
+  tile_coords(tile, e.to, tm, tn);
   const int m0 = tm * BBM, n0 = tn * BBN;
-  const int nk_all = K / 64, nks = (nk_all + ksplit - 1) / ksplit;
+  const int nk_all = K / 64, nks = ksplit > 1 ? (nk_all + ksplit - 1) / ksplit : nk_all;
   const int k0 = split * nks, nk = min(nks, nk_all - k0);   // host: every split non-empty
   if (ksplit > 1) e.out = static_cast<float*>(e.out) + split * e.split_stride;
   PP2BufSrc src;
@@ -999,7 +1000,7 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_mt_kernel(
   int tile = v;
   const int nk = K / 64, k0 = 0;
   int tm, tn;
-  tile_coords(tile, tiles_m, tiles_n, e.ngw, tm, tn);
+  tile_coords(tile, e.to, tm, tn);
   // epilogue LDS (32-row staging per wave, then the LayerNorm-fold statistics table) past
   // stage 0: the next tile's first K-stage lands there during the epilogue
   char* const epb = smem + BSTAGE;
@@ -1050,7 +1051,7 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_mt_kernel(
     // left the K loop: stages are free), under this tile's epilogue
     const bool more = tile + nwg < nt;
     int tm2 = tm, tn2 = tn;
-    if (more) tile_coords(tile + nwg, tiles_m, tiles_n, e.ngw, tm2, tn2);
+    if (more) tile_coords(tile + nwg, e.to, tm2, tn2);
     // issued unconditionally (out-of-range, traffic-free loads after the last tile): the
     // same instruction sequence on both paths keeps the compiler's counted waits for the
     // epilogue's own loads exact, instead of the minimum over a branch merge
@@ -1116,7 +1117,7 @@ __global__ __launch_bounds__(BNT) void gemm_tn_f32_pp2_kernel(
   const int xcd = bid & 7, q = nt >> 3, r = nt & 7;
   const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   int tm, tn;
-  tile_coords(tile, tiles_m, tiles_n, e.ngw, tm, tn);
+  tile_coords(tile, e.to, tm, tn);
   const int m0 = tm * BBM, n0 = tn * BBN;
   PP2BufSrc src;
   pp2b_sources<TR, float>(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane, 0);
@@ -1235,7 +1236,7 @@ __global__ __launch_bounds__(BNT) void gemm_mx8_pp_kernel(
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   int tm, tn;
-  tile_coords(tile, tiles_m, tiles_n, e.ngw, tm, tn);
+  tile_coords(tile, e.to, tm, tn);
   const int m0 = tm * BBM, n0 = tn * BBN;
   MxpSrc src;
   {
@@ -1553,6 +1554,7 @@ void f32_pp2_launch(int M, int N, int K, const float* A, int lda, const float* B
   });
   EpiArgs e = make_epi_args(epi);
   e.ngw = tile_group_width(tiles_n);
+  e.to = make_tile_order(tiles_m, tiles_n, e.ngw);
   int code = EPI_GENERIC;
   if (pp2_fast_epilogue(epi) && epi->out_dtype == VTD_F32 && !epi->lnstat && !epi->statout &&
       !epi->out2) {
@@ -1635,6 +1637,7 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
     pp2_set_attributes();
     EpiArgs e = make_epi_args(epi);
     e.ngw = ngw;
+    e.to = make_tile_order(tiles_m, tiles_n, e.ngw);
     e.tpw = VTD_DIAG ? pp2_tpw() : 1;   // several tiles per workgroup: diagnostic build only
     const int code = pp2_code(epi);
     // transposed accumulators + register-direct epilogue for activation layers (mlp1 -5 %,
@@ -1781,6 +1784,7 @@ int gemm_splitk_launch(int M, int N, int K, const void* A, int lda, const void* 
   EpiArgs pe{};
   pe.out = part; pe.ldo = N; pe.out_dtype = VTD_F32;
   pe.ngw = tile_group_width(tiles_n);
+  pe.to = make_tile_order(tiles_m, tiles_n, pe.ngw);
   pe.split_stride = (int64_t)M * N;
   const bf16_t* a16 = static_cast<const bf16_t*>(A);
   const bf16_t* b16 = static_cast<const bf16_t*>(Bt);
@@ -1829,6 +1833,7 @@ int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_
   ProfScope ps(stream, PROF_GEMM, flops > 0 ? flops : 2.0 * M * N * (double)K);
   const int tiles_m = (M + BBM - 1) / BBM, tiles_n = (N + BBN - 1) / BBN;
   e.ngw = tile_group_width(tiles_n);
+  e.to = make_tile_order(tiles_m, tiles_n, e.ngw);
 #if VTD_DIAG
   // 3: x4 for the long-K layers (K >= 2048: the MLP's inner and last), ping-pong otherwise
   const int mxv = mx_variant();

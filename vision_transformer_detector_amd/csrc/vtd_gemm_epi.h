@@ -3,10 +3,50 @@
 // fold / partial statistics, the head's Reshape scatter and the fused decode.
 #pragma once
 
+#include <algorithm>
+
 #include "vtd_common.h"
 
 namespace vtd {
 namespace {
+
+// n / d for 0 <= n < 2^31 by a multiply-high and a shift (Granlund-Montgomery round-up
+// method: s = ceil(log2 d), m = floor(2^32 (2^s - d) / d) + 1, q = (mulhi(n, m) + n) >> s):
+// the pp2 tile-order divisions otherwise cost ~300 scalar instructions between a workgroup's
+// start and its first DMA
+struct FastDiv {
+  uint32_t m, s;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  const uint64_t m = ((uint64_t(1) << 32) * ((uint64_t(1) << s) - d)) / d + 1;
+  return FastDiv{(uint32_t)m, s};
+}
+__device__ __forceinline__ int fdiv(int n, FastDiv f) {
+  return (int)((__umulhi((uint32_t)n, f.m) + (uint32_t)n) >> f.s);
+}
+// The grouped tile order of EpiArgs::ngw with its divisors precomputed (make_tile_order)
+struct TileOrder {
+  int tiles_n, ngw, full, lw, gsz, grouped;
+  FastDiv f_tn, f_ngw, f_lw, f_gsz;
+};
+inline TileOrder make_tile_order(int tiles_m, int tiles_n, int ngw) {
+  TileOrder t{};
+  t.tiles_n = tiles_n;
+  t.grouped = ngw > 0 && ngw < tiles_n;
+  t.f_tn = make_fastdiv((uint32_t)std::max(tiles_n, 1));
+  if (t.grouped) {
+    t.ngw = ngw;
+    t.full = tiles_n / ngw;
+    t.lw = tiles_n - t.full * ngw;
+    t.gsz = tiles_m * ngw;
+    t.f_ngw = make_fastdiv((uint32_t)ngw);
+    t.f_lw = make_fastdiv((uint32_t)std::max(t.lw, 1));
+    t.f_gsz = make_fastdiv((uint32_t)std::max(t.gsz, 1));
+  }
+  return t;
+}
 
 struct EpiArgs {
   const float* bias;
@@ -40,6 +80,8 @@ struct EpiArgs {
   // pp2 (ksplit == 1): consecutive tiles per workgroup (<= 1: one); with more than one, the
   // next tile's first K-stage is loaded while the current tile's epilogue runs
   int tpw;
+  // the tile order of ngw with precomputed divisors (set with ngw by the 256-tile launchers)
+  TileOrder to;
 };
 
 // bf16 output row vector store of the fast epilogues; build-time A/B knob VTD_OUT_NT: 1 =
@@ -52,6 +94,25 @@ __device__ __forceinline__ void store_out16(void* p, i32x4 v) {
   else *reinterpret_cast<i32x4*>(p) = v;
 }
 
+// tile index -> (tm, tn) for a TileOrder (the same map as the form below, divisions by
+// multiply-high)
+__device__ __forceinline__ void tile_coords(int tile, const TileOrder& t, int& tm, int& tn) {
+  if (!t.grouped) {
+    tm = fdiv(tile, t.f_tn);
+    tn = tile - tm * t.tiles_n;
+    return;
+  }
+  const int g = fdiv(tile, t.f_gsz);
+  if (g < t.full) {
+    const int r = tile - g * t.gsz;
+    tm = fdiv(r, t.f_ngw);
+    tn = g * t.ngw + (r - tm * t.ngw);
+  } else {
+    const int r = tile - t.full * t.gsz;
+    tm = fdiv(r, t.f_lw);
+    tn = t.full * t.ngw + (r - tm * t.lw);
+  }
+}
 // tile index -> (tm, tn) for EpiArgs::ngw (bijective; the last n-group may be narrower)
 __device__ __forceinline__ void tile_coords(int tile, int tiles_m, int tiles_n, int ngw, int& tm,
                                             int& tn) {
