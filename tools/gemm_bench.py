@@ -23,6 +23,11 @@ SHAPES = {  # name: (M, N, K, act, out_dtype, resid)
     "head1": (4352, 8704, 256, 1, 1, False),
     "head2": (4352, 4352, 8704, 1, 1, False),
     "sq8192": (8192, 8192, 8192, 0, 1, False),
+    # the head's skinny-kernel layers per micro-batch half (B = 128: 2176 rows), padded widths
+    "det17": (25088, 17, 768, 0, 1, False),
+    "head272": (2176, 320, 576, 1, 1, False),
+    "head136": (2176, 192, 320, 1, 1, False),
+    "head6": (2176, 6, 192, 0, 0, False),
     # diagnostics: the activation's share of an epilogue (mlp1 / mlp2 without GELU)
     "mlp1_noact": (50176, 3072, 768, 0, 1, False),
     "mlp2_noact": (50176, 1536, 3072, 0, 1, False),

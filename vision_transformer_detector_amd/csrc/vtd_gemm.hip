@@ -172,12 +172,38 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(int M, int N, int K,
       a[j] = *reinterpret_cast<const i32x4*>(ap + min(s0 + j, nks - 1) * 32);
   };
   load(a0, 0);
-  // Bt rows n0 .. n0 + 31: slab t = k / 64, row r, 16-B chunk c at t * 4096 + r * 128 + (c ^ (r & 7)) * 16
-  for (int i = tid; i < 32 * (K >> 3); i += 256) {
-    const int r = i / (K >> 3), cc = i - r * (K >> 3), t = cc >> 3, c = cc & 7;
-    i32x4 v = {0, 0, 0, 0};
-    if (n0 + r < N) v = *reinterpret_cast<const i32x4*>(Bt + (int64_t)(n0 + r) * ldb + cc * 8);
-    *reinterpret_cast<i32x4*>(smem + t * 4096 + r * 128 + ((c ^ (r & 7)) << 4)) = v;
+  // Bt rows n0 .. n0 + 31: slab t = k / 64, row r, 16-B chunk c at t * 4096 + r * 128 + (c ^ (r & 7)) * 16.
+  // Eight chunks per thread in flight at once (a load-store loop waited out one load latency
+  // per chunk: 8-12 serial round trips at the head's K = 544-768); a thread's chunks are
+  // 256 apart, stepped as (row, chunk) without a division per chunk.
+  {
+    const int kc = K >> 3, nch = 32 * kc;
+    const int dr = 256 / kc, dc = 256 - dr * kc;
+    int r0 = tid / kc, c0 = tid - r0 * kc;
+    for (int i0 = tid; i0 < nch; i0 += 8 * 256) {
+      i32x4 v[8];
+      int rr[8], cc[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        rr[u] = r0;
+        cc[u] = c0;
+        v[u] = i32x4{0, 0, 0, 0};
+        if (i0 + u * 256 < nch && n0 + r0 < N)
+          v[u] = *reinterpret_cast<const i32x4*>(Bt + (int64_t)(n0 + r0) * ldb + c0 * 8);
+        r0 += dr;
+        c0 += dc;
+        if (c0 >= kc) {
+          c0 -= kc;
+          ++r0;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (i0 + u * 256 < nch) {
+          const int r = rr[u], t = cc[u] >> 3, c = cc[u] & 7;
+          *reinterpret_cast<i32x4*>(smem + t * 4096 + r * 128 + ((c ^ (r & 7)) << 4)) = v[u];
+        }
+    }
   }
   __syncthreads();
   f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
