@@ -408,7 +408,8 @@ int vtd_profile_read(double* ms, int64_t* launches, double* flops, int n_classes
  *     workgroup target per launch (default 256); both change the workspace size.
  *   VTD_KNOB_JPEG_CHUNK_BITS (VTD_JPEG_CHUNK_BITS): Huffman chunk length of vtd_jpeg_decode.
  *   VTD_KNOB_SKINNY (VTD_SKINNY): 0 keeps the head's narrow bf16 layers (N <= 320) on the
- *     128 x 128 kernel instead of the skinny one.
+ *     128 x 128 kernel instead of the skinny one; a value >= 64 sets the N threshold (such
+ *     layers are then not split-K).
  *   VTD_KNOB_F32_PP2 (VTD_F32_PP2): 0 keeps large fp32-mode GEMMs on the 128 x 128 kernel
  *     instead of the 256-tile f32 one.
  *   VTD_KNOB_STAGGER (VTD_STAGGER): the two-stream split's second micro-batch starts k stages

@@ -1467,9 +1467,12 @@ bool gemm_emits_stats(int M, int N, int dtype, const vtd_epilogue* e) {
 // The skinny kernel for problems the 256-tile kernels do not take (< kMinBigTiles tiles or
 // N <= 64): the head's Dense(17) projection (any M) and its narrow layers, when every
 // 32-column block re-reads A at most 10 times (N <= 320) -- wider layers keep the 128 x 128
-// kernel's A reuse.  VTD_KNOB_SKINNY = 0 disables it.
+// kernel's A reuse.  VTD_KNOB_SKINNY = 0 disables it; a value >= 64 sets the N threshold.
+constexpr int kSkinnyMaxN = 320;
 bool skinny_choice(int M, int N, int K) {
-  return knob(VTD_KNOB_SKINNY) != 0 && N <= 320 && K % 64 == 0 && M > 0;
+  const int kn = knob(VTD_KNOB_SKINNY);
+  const int max_n = kn >= 64 ? kn : kSkinnyMaxN;
+  return kn != 0 && N <= max_n && K % 64 == 0 && M > 0;
 }
 
 // Whether vtd_gemm_mx8 can write its output as MX-fp8 (out_dtype VTD_FP8): the fast
@@ -1779,6 +1782,8 @@ int gemm_splitk_choice(int M, int N, int K, int dtype) {
   const int tiles = ((M + BBM - 1) / BBM) * ((N + BBN - 1) / BBN);
   const int nk = K / 64;
   if (tiles >= (3 * kSplitTarget) / 4) return 1;
+  // a layer the skinny kernel takes (gemm_launch) stays unsplit
+  if (tiles < kMinBigTiles && K <= SK_KMAX && skinny_choice(M, N, K)) return 1;
   const int s = std::min((kSplitTarget + tiles - 1) / tiles, nk / kSplitMinSteps);
   if (s < 2) return 1;
   const int nks = (nk + s - 1) / s;
