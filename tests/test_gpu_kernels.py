@@ -118,12 +118,13 @@ def test_gemm_bf16_output(L, cuda, dtype):
     (25088, 17, 768, 0, 1, False),     # Dense(17) (without the scatter)
     (1000, 100, 2048, 1, 0, True),     # the largest K, ragged M and N, f32 residual
     (33, 64, 64, 2, 1, True),          # one K-step pair, bf16 residual in place
-    (777, 257, 1088, 0, 0, False)])    # ragged column block
-@pytest.mark.parametrize("skinny", [1, 0])
+    (777, 257, 1088, 0, 0, False),     # ragged column block
+    (2176, 576, 1088, 1, 1, False)])   # Dense(544): skinny only with the threshold knob (640)
+@pytest.mark.parametrize("skinny", [1, 0, 640])
 def test_gemm_skinny(L, cuda, M, N, K, act, out_dtype, resid, skinny):
-    """The skinny bf16 kernel (N <= 320, below the 256-tile threshold) against fp64, and the
-    128 x 128 kernel it replaces (knob VTD_KNOB_SKINNY = 0): both fp32 accumulation of bf16
-    products, so they agree to fp32 summation order."""
+    """The skinny bf16 kernel (N <= 320, below the 256-tile threshold; knob value 640 raises the
+    threshold) against fp64, and the 128 x 128 kernel it replaces (knob VTD_KNOB_SKINNY = 0):
+    both fp32 accumulation of bf16 products, so they agree to fp32 summation order."""
     g = torch.Generator(device=cuda).manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
     Bt = (torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
