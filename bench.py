@@ -83,9 +83,10 @@ def traffic_per_launch():
     this same bench command), or None when no such measurement exists."""
     p = os.path.join(ROOT, "profiles", "gemm_traffic_latest.json")
     try:
-        return round(json.load(open(p))["traffic_bytes_per_launch"])
+        j = json.load(open(p))
+        return round(j["traffic_bytes_per_launch"]), j.get("source", "see the file")
     except (OSError, KeyError, ValueError):
-        return None
+        return None, None
 
 
 def gemm_alg_bytes(kw, dims, b, rb=2):
@@ -411,6 +412,9 @@ def main():
     g = kernels["gemm"]
     gemm_tf = g["tflops"]
     headline = args.preset == "vit_b16_224" and B == 256 and args.dtype == "bf16"
+    # the committed PMC passes are of the headline command (C2, B = 256, bf16)
+    headline_cfg = headline
+    traffic, traffic_src = traffic_per_launch()
     metric = ("images/sec ViT-B/16 detector fwd, batch 256, 1/2/4/8 MI355X; MFMA util %"
               if headline else
               f"images/sec {args.preset} detector fwd, batch {B} per GPU, {args.dtype}, "
@@ -443,9 +447,10 @@ def main():
                      "achieved": round(gemm_tf, 1) if gemm_tf else None, "peak": peak,
                      "unit": "TFLOP/s",
                      "frac": round(gemm_tf / peak, 4) if gemm_tf else None,
-                     # the committed PMC passes are of the headline command (C2, B = 256, bf16)
-                     "traffic": traffic_per_launch() if (args.preset == "vit_b16_224" and
-                                                         args.dtype == "bf16" and B == 256)
+                     "traffic": traffic if headline_cfg else None,
+                     "traffic_source": (f"profiles/gemm_traffic_latest.json ({traffic_src}): "
+                                        "rocprofv3 PMC passes of this command on a builder box, "
+                                        "not measured in this run") if headline_cfg and traffic
                      else None,
                      "algorithmic_bytes_per_launch": round(gemm_alg_bytes(
                          kw, model.dims, B, 4 if (args.dtype in ("f32", "float32") or

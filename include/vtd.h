@@ -325,21 +325,29 @@ int vtd_jpeg_decode(const uint8_t* const* jpegs, const size_t* lens, int n, uint
  * :431) as TF's libpng path does it: every colour type and bit depth (1-16), Adam7
  * interlacing; palette -> RGB, gray -> RGB, alpha / tRNS dropped, 16-bit -> high byte.  The
  * chunk walk (critical-chunk CRCs checked) and the zlib inflate run on the host over a few
- * threads; the filtered scanlines are copied to the workspace on `stream` (pinned staging the
- * library reuses) and un-filtered + converted on the device, image i written as RGB uint8 HWC
- * at out_dev + out_offsets[i].  Same calling convention as the JPEG entry points;
- * vtd_png_info's comps = samples per pixel of the file (1-4). */
+ * threads; a row filter byte above 4 is an error (libpng's "bad adaptive filter value"); the
+ * filtered scanlines are copied to the workspace on `stream` (pinned staging the library
+ * reuses) and un-filtered + converted on the device (rows of up to 16 KiB of filtered bytes
+ * through LDS, wider ones in place in the workspace: no width limit beyond w * h <= 2^28),
+ * image i written as RGB uint8 HWC at out_dev + out_offsets[i].  Same calling convention as
+ * the JPEG entry points; vtd_png_info's comps = samples per pixel of the file (1-4).
+ * vtd_png_inflate: the host half alone for one file (chunk walk, inflate, filter-byte check)
+ * into a caller HOST buffer; *need = the filtered scanline bytes of all passes (out == NULL:
+ * only *need). */
 int vtd_png_info(const uint8_t* png, size_t len, int* h, int* w, int* comps);
 int vtd_png_workspace_bytes(const uint8_t* const* pngs, const size_t* lens, int n,
                             int32_t* dims, size_t* bytes);
 int vtd_png_decode(const uint8_t* const* pngs, const size_t* lens, int n, uint8_t* out_dev,
                    const int64_t* out_offsets, void* workspace_dev, size_t workspace_bytes,
                    void* stream);
+int vtd_png_inflate(const uint8_t* png, size_t len, uint8_t* out, size_t out_bytes, size_t* need);
 
-/* BMP decode, tf.image.decode_image(file, channels=3) for BMP as TF's decode_bmp does it:
- * 24-bit uncompressed rows (bottom-up, or top-down for a negative height), BGR -> RGB; other
- * bit depths are refused as TF refuses a bits-per-pixel / channels mismatch.  Same calling
- * convention as the PNG / JPEG entry points. */
+/* BMP decode, tf.image.decode_image(file, channels=3) for BMP as TF 2.x's DecodeImageV2 does it
+ * (decode_image_op.cc): the file's channels = bits-per-pixel / 8 in {1, 3, 4}, rows bottom-up
+ * (top-down for a negative height) padded to 4 bytes; 24-bit BGR -> RGB, 32-bit BGRA -> RGB
+ * (alpha dropped), 8-bit -> the stored byte replicated (TF applies no palette).  Other bit
+ * depths and RLE compression (which TF would misread) return VTD_ERR_UNSUPPORTED.  Same
+ * calling convention as the PNG / JPEG entry points; comps = 3. */
 int vtd_bmp_info(const uint8_t* bmp, size_t len, int* h, int* w, int* comps);
 int vtd_bmp_workspace_bytes(const uint8_t* const* bmps, const size_t* lens, int n,
                             int32_t* dims, size_t* bytes);

@@ -5,9 +5,13 @@
 // entry point (rejected before any device call), the profiling state -- re-expressed in
 // C++ so the instrumented code runs without preloading the sanitizer runtime into Python.
 // No GPU is touched: every compute call below fails argument validation first.
+#include <zlib.h>
+
+#include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <initializer_list>
+#include <string>
 #include <vector>
 
 #include "vtd.h"
@@ -84,6 +88,116 @@ static const uint8_t kJpegProg[] = {
     1,0,17,33,97,240,49,65,81,255,218,0,8,1,1,0,1,63,16,101,25,7,133,75,116,52,182,202,226,172,97,
     253,129,3,246,115,147,58,111,145,213,224,159,255,217,
 };
+
+// ---- PNG / BMP files built here (the parsers' inputs are untrusted file bytes)
+typedef std::vector<uint8_t> Bytes;
+static void put_be32(Bytes& b, uint32_t v) {
+  for (int s = 24; s >= 0; s -= 8) b.push_back((uint8_t)(v >> s));
+}
+static void put_le(Bytes& b, uint32_t v, int n) {
+  for (int i = 0; i < n; ++i) b.push_back((uint8_t)(v >> (8 * i)));
+}
+static Bytes png_chunk(const char* type, const Bytes& body, bool good_crc = true) {
+  Bytes c;
+  put_be32(c, (uint32_t)body.size());
+  c.insert(c.end(), type, type + 4);
+  c.insert(c.end(), body.begin(), body.end());
+  uLong crc = crc32(0L, Z_NULL, 0);
+  crc = crc32(crc, c.data() + 4, (uInt)(4 + body.size()));
+  put_be32(c, good_crc ? (uint32_t)crc : (uint32_t)crc ^ 1u);
+  return c;
+}
+static Bytes png_ihdr(uint32_t w, uint32_t h, int depth, int ctype, int interlace) {
+  Bytes b;
+  put_be32(b, w);
+  put_be32(b, h);
+  b.push_back((uint8_t)depth); b.push_back((uint8_t)ctype);
+  b.push_back(0); b.push_back(0); b.push_back((uint8_t)interlace);
+  return b;
+}
+static Bytes zcompress(const Bytes& raw) {
+  uLongf n = compressBound((uLong)raw.size());
+  Bytes out(n);
+  compress(out.data(), &n, raw.data(), (uLong)raw.size());
+  out.resize(n);
+  return out;
+}
+// an RGB8 w x h PNG whose rows carry filter types 0..4 in turn; extra: chunks before IDAT
+static Bytes make_png(int w, int h, const Bytes& extra = Bytes(), int bad_filter_row = -1) {
+  Bytes raw;
+  for (int r = 0; r < h; ++r) {
+    raw.push_back((uint8_t)(r == bad_filter_row ? 9 : r % 5));
+    for (int i = 0; i < 3 * w; ++i) raw.push_back((uint8_t)(r * 31 + i * 7));
+  }
+  static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', 0x0D, 0x0A, 0x1A, 0x0A};
+  Bytes f(sig, sig + 8);
+  const Bytes ihdr = png_chunk("IHDR", png_ihdr(w, h, 8, 2, 0));
+  f.insert(f.end(), ihdr.begin(), ihdr.end());
+  f.insert(f.end(), extra.begin(), extra.end());
+  const Bytes idat = png_chunk("IDAT", zcompress(raw));
+  f.insert(f.end(), idat.begin(), idat.end());
+  const Bytes iend = png_chunk("IEND", Bytes());
+  f.insert(f.end(), iend.begin(), iend.end());
+  return f;
+}
+// PNG with an arbitrary IHDR and IDAT payload
+static Bytes png_raw(const Bytes& ihdr_body, const Bytes& idat_body, const Bytes& extra = Bytes()) {
+  static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', 0x0D, 0x0A, 0x1A, 0x0A};
+  Bytes f(sig, sig + 8);
+  for (const Bytes& c : {png_chunk("IHDR", ihdr_body), extra, png_chunk("IDAT", idat_body),
+                         png_chunk("IEND", Bytes())})
+    f.insert(f.end(), c.begin(), c.end());
+  return f;
+}
+// host decode path of one file: info, workspace planning, inflate into an exactly sized buffer
+static int png_host(const Bytes& f) {
+  int h = 0, w = 0, c = 0;
+  const int rc = vtd_png_info(f.data(), f.size(), &h, &w, &c);
+  const uint8_t* pp[1] = {f.data()};
+  size_t pl[1] = {f.size()};
+  int32_t pd[2];
+  size_t pb = 0, need = 0;
+  (void)vtd_png_workspace_bytes(pp, pl, 1, pd, &pb);
+  if (vtd_png_inflate(f.data(), f.size(), nullptr, 0, &need) != VTD_OK) return rc ? rc : -100;
+  if (need > ((size_t)1 << 26)) return rc;        // plan only (no 2^28-pixel buffers here)
+  Bytes out(need);
+  const int ri = vtd_png_inflate(f.data(), f.size(), out.data(), out.size(), &need);
+  return rc ? rc : ri;
+}
+static Bytes make_bmp(int32_t w, int32_t h, int bpp, uint32_t pix_off = 0, int32_t comp = 0,
+                      int pixel_bytes = -1) {
+  const int ncol = bpp == 8 ? 256 : 0;
+  const uint32_t off = pix_off ? pix_off : 54 + 4 * ncol;
+  const int64_t rows = h < 0 ? -(int64_t)h : h;
+  const int64_t row = ((int64_t)bpp * (w > 0 ? w : 0) + 31) / 32 * 4;
+  const int64_t pix = pixel_bytes >= 0 ? pixel_bytes : row * rows;
+  Bytes b;
+  b.push_back('B'); b.push_back('M');
+  put_le(b, (uint32_t)(54 + 4 * ncol + pix), 4);
+  put_le(b, 0, 4);
+  put_le(b, off, 4);
+  put_le(b, 40, 4);
+  put_le(b, (uint32_t)w, 4);
+  put_le(b, (uint32_t)h, 4);
+  put_le(b, 1, 2);
+  put_le(b, (uint32_t)bpp, 2);
+  put_le(b, (uint32_t)comp, 4);
+  for (int i = 0; i < 5; ++i) put_le(b, 0, 4);
+  for (int i = 0; i < 4 * ncol; ++i) b.push_back((uint8_t)i);
+  for (int64_t i = 0; i < pix; ++i) b.push_back((uint8_t)(i * 13));
+  return b;
+}
+static int bmp_host(const Bytes& f) {
+  int h = 0, w = 0, c = 0;
+  const int rc = vtd_bmp_info(f.data(), f.size(), &h, &w, &c);
+  const uint8_t* pp[1] = {f.data()};
+  size_t pl[1] = {f.size()};
+  int32_t pd[2];
+  size_t pb = 0;
+  const int rw = vtd_bmp_workspace_bytes(pp, pl, 1, pd, &pb);
+  CHECK((rc == VTD_OK) == (rw == VTD_OK));
+  return rc;
+}
 
 int main() {
   CHECK(vtd_abi_version() == VTD_ABI_VERSION);
@@ -209,6 +323,96 @@ int main() {
       size_t pb = 0;
       (void)vtd_jpeg_workspace_bytes(pp, pl, 1, pd, &pb);
     }
+  }
+  // PNG host side: every truncation, bad CRCs, IHDR size edges, short and
+  // garbage zlib streams, long PLTE, bad filter bytes (exactly sized copies throughout)
+  {
+    const Bytes good = make_png(13, 9);
+    CHECK(png_host(good) == VTD_OK);
+    for (size_t cut = 0; cut < good.size(); ++cut) {
+      Bytes part(good.begin(), good.begin() + cut);
+      CHECK(png_host(part) != VTD_OK);
+    }
+    for (size_t i = 8; i < good.size(); ++i) {            // every byte flipped: CRC / structure
+      Bytes bad = good;
+      bad[i] ^= 0x41;
+      (void)png_host(bad);
+    }
+    Bytes badcrc = make_png(13, 9, png_chunk("PLTE", Bytes(30, 7), false));
+    CHECK(png_host(badcrc) != VTD_OK);
+    // IHDR sizes: 2^28 pixels accepted (planned only), one more refused; 32-bit products and
+    // widths >= 2^31 refused
+    Bytes one(1, 0);
+    int h = 0, w = 0, c = 0;
+    const Bytes edge = png_raw(png_ihdr(1u << 14, 1u << 14, 8, 2, 0), zcompress(one));
+    CHECK(vtd_png_info(edge.data(), edge.size(), &h, &w, &c) == VTD_OK);
+    for (uint32_t ww : {(1u << 14) + 1u, 1u << 16, 0x80000000u, 0xFFFFFFFFu}) {
+      const Bytes f = png_raw(png_ihdr(ww, ww == (1u << 14) + 1 ? 1u << 14 : ww, 8, 2, 0),
+                              zcompress(one));
+      CHECK(vtd_png_info(f.data(), f.size(), &h, &w, &c) != VTD_OK);
+    }
+    const Bytes ovf = png_raw(png_ihdr(0x10000u, 0x10000u, 16, 6, 1), zcompress(one));
+    CHECK(vtd_png_info(ovf.data(), ovf.size(), &h, &w, &c) != VTD_OK);
+    const Bytes zero = png_raw(png_ihdr(0, 5, 8, 2, 0), zcompress(one));
+    CHECK(vtd_png_info(zero.data(), zero.size(), &h, &w, &c) != VTD_OK);
+    // zlib: garbage, every prefix of a valid stream, a valid stream that is too short
+    Bytes raw;
+    for (int r = 0; r < 6; ++r) {
+      raw.push_back(1);
+      for (int i = 0; i < 15; ++i) raw.push_back((uint8_t)(i * r));
+    }
+    const Bytes z = zcompress(raw);
+    CHECK(png_host(png_raw(png_ihdr(5, 6, 8, 2, 0), z)) == VTD_OK);
+    // (a stream cut inside its trailing Adler-32, or just before the final block's
+    // end-of-block code, has delivered every image byte: accepted, the image data is complete;
+    // every shorter prefix is refused)
+    for (size_t cut = 0; cut < z.size(); ++cut) {
+      const int rc = png_host(png_raw(png_ihdr(5, 6, 8, 2, 0), Bytes(z.begin(), z.begin() + cut)));
+      if (cut + 5 < z.size()) CHECK(rc != VTD_OK);
+    }
+    Bytes garbage(64);
+    for (size_t i = 0; i < garbage.size(); ++i) garbage[i] = (uint8_t)(i * 97 + 13);
+    CHECK(png_host(png_raw(png_ihdr(5, 6, 8, 2, 0), garbage)) != VTD_OK);
+    CHECK(png_host(png_raw(png_ihdr(5, 7, 8, 2, 0), z)) != VTD_OK);   // one row short
+    // PLTE: longer than 768 bytes, not a multiple of 3, empty
+    for (size_t n : {size_t(771), size_t(769), size_t(0), size_t(768)}) {
+      const Bytes f = make_png(4, 4, png_chunk("PLTE", Bytes(n, 9)));
+      if (n == 768) CHECK(png_host(f) == VTD_OK);
+      else CHECK(png_host(f) != VTD_OK);
+    }
+    // a filter-type byte above 4
+    const Bytes bf = make_png(6, 5, Bytes(), 3);
+    CHECK(png_host(bf) != VTD_OK);
+    CHECK(std::string(vtd_last_error()).find("filter") != std::string::npos);
+    size_t need = 0;
+    CHECK(vtd_png_inflate(good.data(), good.size(), nullptr, 0, &need) == VTD_OK && need > 0);
+    Bytes small(need - 1);
+    CHECK(vtd_png_inflate(good.data(), good.size(), small.data(), small.size(), &need) ==
+          VTD_ERR_WORKSPACE);
+  }
+  // BMP host side: 8 / 24 / 32-bit, negative (top-down) heights, zero heights, bad offsets,
+  // RLE, every truncation
+  {
+    for (int bpp : {8, 24, 32}) {
+      CHECK(bmp_host(make_bmp(7, 5, bpp)) == VTD_OK);
+      CHECK(bmp_host(make_bmp(7, -5, bpp)) == VTD_OK);
+      CHECK(bmp_host(make_bmp(7, 0, bpp)) != VTD_OK);
+      CHECK(bmp_host(make_bmp(0, 5, bpp)) != VTD_OK);
+      CHECK(bmp_host(make_bmp(-7, 5, bpp)) != VTD_OK);
+      CHECK(bmp_host(make_bmp(7, INT32_MIN, bpp, 0, 0, 0)) != VTD_OK);
+      CHECK(bmp_host(make_bmp(7, 5, bpp, 20)) != VTD_OK);                // offset inside the header
+      CHECK(bmp_host(make_bmp(7, 5, bpp, 0x7FFFFFF0u)) != VTD_OK);       // offset past the file
+      CHECK(bmp_host(make_bmp(7, 5, bpp, 0xFFFFFFF0u)) != VTD_OK);       // negative offset
+      CHECK(bmp_host(make_bmp(7, 5, bpp, 0, 0, 10)) != VTD_OK);          // short pixel array
+      CHECK(bmp_host(make_bmp(1 << 15, 1 << 14, bpp, 0, 0, 0)) != VTD_OK);   // 2^29 pixels
+      CHECK(bmp_host(make_bmp(0x7FFFFFFF, 2, bpp, 0, 0, 0)) != VTD_OK);
+      const Bytes f = make_bmp(9, -3, bpp);
+      for (size_t cut = 0; cut < f.size(); ++cut)
+        CHECK(bmp_host(Bytes(f.begin(), f.begin() + cut)) != VTD_OK);
+    }
+    CHECK(bmp_host(make_bmp(7, 5, 8, 0, 1)) != VTD_OK);                  // RLE8
+    CHECK(bmp_host(make_bmp(7, 5, 16)) != VTD_OK);
+    CHECK(bmp_host(make_bmp(7, 5, 32, 0, 3)) == VTD_OK);                 // BI_BITFIELDS
   }
   // profiling state (host only)
   CHECK(vtd_profile_reset() == VTD_OK);

@@ -169,6 +169,41 @@ def test_png_pillow_files_and_mixed_batch(cuda):
         assert np.array_equal(mine, ref), i
 
 
+def test_png_wide_rows_bit_exact(cuda):
+    """Rows wider than the LDS row buffer (16 KiB of filtered bytes) are unfiltered in place in
+    the workspace: RGB8 6000 px (18,000 B rows), RGBA16 2100 px interlaced (Adam7's last passes
+    are the wide ones), gray 1-bit 150,000 px, next to a narrow file in the same batch; every
+    filter type on every row."""
+    from vision_transformer_detector_amd.preprocess import decode_images
+    files, refs = [], []
+    for i, (h, w, ctype, depth, il) in enumerate([(6, 6000, 2, 8, False), (9, 2100, 6, 16, True),
+                                                  (5, 150000, 0, 1, False), (17, 23, 2, 8, False)]):
+        f, ref = _case(40 + i, h, w, ctype, depth, il)
+        files.append(f)
+        refs.append(ref)
+    pixels, offsets, sizes = decode_images(files, device=cuda)
+    torch.cuda.synchronize()
+    got = pixels.cpu().numpy()
+    for i, ref in enumerate(refs):
+        h, w = sizes[i]
+        mine = got[offsets[i]:offsets[i] + h * w * 3].reshape(h, w, 3)
+        assert np.array_equal(mine, ref), i
+
+
+def test_png_bad_filter_type_raises(cuda):
+    """A row filter byte above 4 is an error (libpng: bad adaptive filter value), not a row
+    decoded as None."""
+    from vision_transformer_detector_amd.preprocess import decode_images
+    samples = np.arange(4 * 5 * 3).reshape(4, 5, 3) % 256
+    raw = bytearray(zlib.decompress(zlib.compress(
+        _filter_rows(_pack_rows(samples.reshape(4, -1), 8), 3, 0))))
+    raw[2 * (1 + 15)] = 7                                       # row 2's filter byte
+    f = (b"\x89PNG\r\n\x1a\n" + _chunk(b"IHDR", struct.pack(">IIBBBBB", 5, 4, 8, 2, 0, 0, 0)) +
+         _chunk(b"IDAT", zlib.compress(bytes(raw))) + _chunk(b"IEND", b""))
+    with pytest.raises((ValueError, RuntimeError), match="filter"):
+        decode_images([f], device=cuda)
+
+
 def test_png_corrupt_stream_raises(cuda):
     from vision_transformer_detector_amd.preprocess import decode_images
     f, _ = _case(0, *CASES[0])
@@ -181,7 +216,7 @@ def test_png_corrupt_stream_raises(cuda):
 
 
 def test_bmp_decode_bottom_up_and_top_down(cuda):
-    """24-bit BMP (TF decode_bmp): bottom-up rows from Pillow's encoder and the same file made
+    """24-bit BMP (TF decode_image): bottom-up rows from Pillow's encoder and the same file made
     top-down (negative height, rows reversed), widths with 4-byte row padding."""
     from vision_transformer_detector_amd.preprocess import decode_images
     files, refs = [], []
@@ -199,6 +234,41 @@ def test_bmp_decode_bottom_up_and_top_down(cuda):
         td[22:26] = (-h).to_bytes(4, "little", signed=True)
         files.append(bytes(td))
         refs.append(rgb)
+    pixels, offsets, sizes = decode_images(files, device=cuda)
+    torch.cuda.synchronize()
+    got = pixels.cpu().numpy()
+    for i, ref in enumerate(refs):
+        h, w = sizes[i]
+        assert np.array_equal(got[offsets[i]:offsets[i] + h * w * 3].reshape(h, w, 3), ref), i
+
+
+def test_bmp_decode_8_and_32_bit(cuda):
+    """8- and 32-bit BMP as TF 2.x decode_image (decode_image_op.cc DecodeBmpV2) converts them to
+    channels = 3: 32-bit BGRA -> RGB (alpha dropped); 8-bit -> the stored byte replicated into
+    R, G, B -- the palette is not applied (a Pillow "P" file with a non-identity palette
+    decodes to its indices), which is what TF's decoder does.  Parity against TF itself is
+    unpinned (not importable here)."""
+    from vision_transformer_detector_amd.preprocess import decode_images
+    rng = np.random.default_rng(5)
+    files, refs = [], []
+    for k, (h, w) in enumerate([(7, 13), (5, 3), (20, 31)]):
+        rgba = rng.integers(0, 256, (h, w, 4), dtype=np.uint8)
+        b = io.BytesIO()
+        Image.fromarray(rgba, mode="RGBA").save(b, format="BMP")
+        files.append(b.getvalue())
+        refs.append(rgba[..., :3])
+        gray = rng.integers(0, 256, (h, w), dtype=np.uint8)
+        b = io.BytesIO()
+        Image.fromarray(gray, mode="L").save(b, format="BMP")
+        files.append(b.getvalue())
+        refs.append(np.repeat(gray[..., None], 3, -1))
+        idx = rng.integers(0, 16, (h, w), dtype=np.uint8)
+        im = Image.fromarray(idx, mode="P")
+        im.putpalette(list(rng.integers(0, 256, 16 * 3).astype(int)))
+        b = io.BytesIO()
+        im.save(b, format="BMP")
+        files.append(b.getvalue())
+        refs.append(np.repeat(idx[..., None], 3, -1))
     pixels, offsets, sizes = decode_images(files, device=cuda)
     torch.cuda.synchronize()
     got = pixels.cpu().numpy()

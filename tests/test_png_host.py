@@ -76,25 +76,50 @@ def test_png_refusals_name_the_reason(L):
     assert rc != 0 and b"image 1" in L.lib.vtd_last_error()
 
 
+def _bmp(arr, mode):
+    b = io.BytesIO()
+    Image.fromarray(arr).convert(mode).save(b, format="BMP")
+    return b.getvalue()
+
+
 def test_bmp_header_and_refusals(L):
-    """BMP (TF decode_bmp): 24-bit files pass; 32-bit and 8-bit are refused as TF refuses a
-    bits-per-pixel / channels mismatch for channels = 3."""
+    """BMP as TF 2.x's decode_image (DecodeImageV2, decode_image_op.cc): 8-, 24- and 32-bit files
+    pass (channels = bpp / 8 in 1, 3, 4); other depths and RLE compression are refused by name;
+    truncation is refused."""
     rng = np.random.default_rng(1)
     rgb = rng.integers(0, 256, (7, 11, 3), dtype=np.uint8)
-    b = io.BytesIO()
-    Image.fromarray(rgb).save(b, format="BMP")
-    f = b.getvalue()
     h, w, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-    assert L.lib.vtd_bmp_info(f, len(f), ctypes.byref(h), ctypes.byref(w), ctypes.byref(c)) == 0
-    assert (h.value, w.value, c.value) == (7, 11, 3)
-    for mode in ("RGBA", "L"):
-        b = io.BytesIO()
-        Image.fromarray(rgb).convert(mode).save(b, format="BMP")
-        g = b.getvalue()
-        assert L.lib.vtd_bmp_info(g, len(g), ctypes.byref(h), ctypes.byref(w), ctypes.byref(c)) != 0
-        assert b"bits-per-pixel" in L.lib.vtd_last_error()
+    for mode in ("RGB", "RGBA", "L", "P"):
+        f = _bmp(rgb, mode)
+        assert L.lib.vtd_bmp_info(f, len(f), ctypes.byref(h), ctypes.byref(w), ctypes.byref(c)) == 0, \
+            (mode, L.lib.vtd_last_error())
+        assert (h.value, w.value, c.value) == (7, 11, 3)
+    f = _bmp(rgb, "RGB")
+    g = bytearray(f)
+    g[28:30] = (16).to_bytes(2, "little")
+    assert L.lib.vtd_bmp_info(bytes(g), len(g), ctypes.byref(h), ctypes.byref(w), ctypes.byref(c)) != 0
+    assert b"16-bit" in L.lib.vtd_last_error()
+    g = bytearray(_bmp(rgb, "L"))
+    g[30:34] = (1).to_bytes(4, "little")                       # BI_RLE8
+    assert L.lib.vtd_bmp_info(bytes(g), len(g), ctypes.byref(h), ctypes.byref(w), ctypes.byref(c)) != 0
+    assert b"RLE" in L.lib.vtd_last_error()
     assert L.lib.vtd_bmp_info(f[:60], 60, ctypes.byref(h), ctypes.byref(w), ctypes.byref(c)) != 0
     assert b"truncated" in L.lib.vtd_last_error()
+
+
+def test_png_wide_rows_accepted(L):
+    """Rows wider than the decoder's LDS row buffer (16 KiB of filtered bytes: RGB8 wider than
+    5461 px, RGBA16 wider than 2048 px) are accepted by the header walk (they are unfiltered in
+    place on the device); only the 2^28-pixel cap remains."""
+    sig = b"\x89PNG\r\n\x1a\n"
+    for w, depth, ctype in ((6000, 8, 2), (2100, 16, 6), (20000, 1, 0)):
+        ihdr = _chunk(b"IHDR", struct.pack(">IIBBBBB", w, 2, depth, ctype, 0, 0, 0))
+        f = sig + ihdr + _chunk(b"IDAT", zlib.compress(b"")) + _chunk(b"IEND", b"")
+        rc, dims = _info(L, f)
+        assert rc == 0 and dims[:2] == (2, w), L.lib.vtd_last_error()
+    ihdr = _chunk(b"IHDR", struct.pack(">IIBBBBB", 1 << 15, (1 << 13) + 1, 8, 2, 0, 0, 0))
+    f = sig + ihdr + _chunk(b"IEND", b"")
+    assert _info(L, f)[0] != 0 and b"2^28" in L.lib.vtd_last_error()
 
 
 def test_decode_images_routes_by_signature():

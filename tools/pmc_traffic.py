@@ -34,9 +34,10 @@ def main():
            "launches_write_pass": nw, "fetch_bytes_per_launch": fb,
            "write_bytes_per_launch": wb, "traffic_bytes_per_launch": fb + wb,
            "correction": "FETCH_SIZE x 2 (gfx950 wide-read undercount), WRITE_SIZE x 1; KiB"}
-    print(json.dumps(out))
     if len(sys.argv) > 3:
+        out["source"] = sys.argv[3]        # bench.py names it in roofline.traffic_source
         json.dump(out, open(sys.argv[3], "w"), indent=1)
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":

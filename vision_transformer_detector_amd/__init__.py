@@ -8,10 +8,21 @@ All arithmetic runs in hand-written gfx950 HIP kernels in `libvtd.so` (C-ABI:
 """
 import os as _os
 
-# Kernel arguments in device memory (HIP runtime option; +1.8 % on the C2 forward,
-# profiles/r04_dev_kernarg_ab.log).  Takes effect only if the HIP runtime has not been
-# initialised yet in this process; an explicit setting by the caller wins.
-_os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
+def enable_device_kernel_arguments() -> bool:
+    """Opt-in: kernel arguments in device memory (the HIP runtime's HIP_FORCE_DEV_KERNARG=1;
+    +1.8 % on the C2 forward, profiles/r04_dev_kernarg_ab.log).  It changes how EVERY HIP
+    kernel of the process receives its arguments and is read once, when the HIP runtime
+    initialises, so call this before anything touches the GPU (bench.py and
+    __graft_entry__.smoke do); an explicit HIP_FORCE_DEV_KERNARG setting wins.  Returns
+    whether the setting is now on.  VTD_DEV_KERNARG=1 in the environment does the same at
+    import time."""
+    _os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+    return _os.environ["HIP_FORCE_DEV_KERNARG"] == "1"
+
+
+if _os.environ.get("VTD_DEV_KERNARG", "0") == "1":
+    enable_device_kernel_arguments()
 
 from .detector import (Constants, Model, create_vision_transformer_detector,  # noqa: F401
                        decode_detections, detection_list, keras_default_init,
@@ -22,4 +33,5 @@ from .preprocess import get_image_tensors  # noqa: F401
 
 __all__ = ["Constants", "Model", "create_vision_transformer_detector",
            "transform_predictions", "decode_detections", "detection_list", "presets",
-           "MeanAveragePrecision", "iou_calculator", "get_image_tensors"]
+           "MeanAveragePrecision", "iou_calculator", "get_image_tensors",
+           "enable_device_kernel_arguments"]

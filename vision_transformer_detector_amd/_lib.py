@@ -134,6 +134,7 @@ SIGNATURES = {
                                         ctypes.POINTER(c_size_t)]),
     "vtd_png_decode": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                                c_size_t, c_void_p]),
+    "vtd_png_inflate": (c_int, [c_void_p, c_size_t, c_void_p, c_size_t, ctypes.POINTER(c_size_t)]),
     "vtd_bmp_info": (c_int, [c_void_p, c_size_t, ctypes.POINTER(c_int), ctypes.POINTER(c_int),
                              ctypes.POINTER(c_int)]),
     "vtd_bmp_workspace_bytes": (c_int, [c_void_p, c_void_p, c_int, c_void_p,

@@ -30,7 +30,9 @@
 namespace vtd {
 namespace {
 
-constexpr int kPngMaxRow = 16384;   // filtered bytes per row (e.g. 4096 RGBA-8 / 2048 RGBA-16 px)
+// filtered bytes per row staged through LDS (e.g. 4096 RGBA-8 / 2048 RGBA-16 px); wider rows
+// are unfiltered in place in the workspace (no width limit beyond the 2^28-pixel cap)
+constexpr int kPngMaxRow = 16384;
 constexpr int kPngThreads = 256;
 
 struct PngDesc {
@@ -58,15 +60,41 @@ __device__ __forceinline__ int paeth(int a, int b, int c) {
   return (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c);
 }
 
+// Undo one row's filter (PNG spec 9.2) in c, u = the unfiltered row above (all zero for a
+// pass's first row); c / u are LDS rows or, for rows wider than kPngMaxRow, the rows in place
+// in the workspace.  Up runs in parallel, Sub / Average / Paeth serially per byte lane.
+template <typename P, typename Q>
+__device__ __forceinline__ void png_unfilter_row(P c, Q u, bool has_u, int ft, int rb, int bpp,
+                                                 int t) {
+  if (ft == 2) {                                   // Up
+    if (has_u)
+      for (int i = t; i < rb; i += kPngThreads) c[i] = (uint8_t)(c[i] + u[i]);
+  } else if (ft == 1 || ft == 3 || ft == 4) {      // Sub / Average / Paeth
+    if (t < bpp) {
+      int a = 0, cc = 0;                           // left and upper-left of this byte lane
+      for (int i = t; i < rb; i += bpp) {
+        const int b = has_u ? u[i] : 0;
+        const int pred = ft == 1 ? a : ft == 3 ? (a + b) >> 1 : paeth(a, b, cc);
+        a = (uint8_t)(c[i] + pred);
+        c[i] = (uint8_t)a;
+        cc = b;
+      }
+    }
+  }
+}
+
+// One workgroup per image.  Rows of at most kPngMaxRow filtered bytes are staged through
+// LDS (two row buffers); wider rows are unfiltered in place in the workspace (the row above
+// is then the already-unfiltered previous row of the same pass, ordered by the barrier).
 __global__ __launch_bounds__(kPngThreads) void png_unfilter_kernel(const PngDesc* __restrict__ descs,
-                                                                   const uint8_t* __restrict__ data,
+                                                                   uint8_t* __restrict__ data,
                                                                    uint8_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t rows[2][kPngMaxRow + 16];
   __shared__ uint8_t pal[256 * 3];
   const PngDesc& d = descs[blockIdx.x];
   const int t = threadIdx.x;
   for (int i = t; i < 256 * 3; i += kPngThreads) pal[i] = d.pal[i];
-  const uint8_t* src = data + d.data_off;
+  uint8_t* src = data + d.data_off;
   uint8_t* dst = out + d.out_off;
   const int npass = d.interlace ? 7 : 1;
   const int bpp = d.bpp, depth = d.depth, ch = d.channels;
@@ -77,28 +105,21 @@ __global__ __launch_bounds__(kPngThreads) void png_unfilter_kernel(const PngDesc
     const int ph = d.h > y0 ? (d.h - y0 + dy - 1) / dy : 0;
     if (pw == 0 || ph == 0) continue;              // uniform: every thread skips
     const int rb = (int)row_bytes(pw, ch, depth);
+    const bool wide = rb > kPngMaxRow;             // uniform
     int cur = 0;
     __syncthreads();
-    for (int i = t; i < rb; i += kPngThreads) rows[1][i] = 0;    // the row above the first
     for (int r = 0; r < ph; ++r, src += 1 + rb, cur ^= 1) {
-      uint8_t* c = rows[cur];
-      const uint8_t* u = rows[cur ^ 1];
       const int ft = src[0];
-      for (int i = t; i < rb; i += kPngThreads) c[i] = src[1 + i];
-      __syncthreads();
-      if (ft == 2) {                                   // Up
-        for (int i = t; i < rb; i += kPngThreads) c[i] = (uint8_t)(c[i] + u[i]);
-      } else if (ft == 1 || ft == 3 || ft == 4) {      // Sub / Average / Paeth: serial per byte lane
-        if (t < bpp) {
-          int a = 0, cc = 0;                           // left and upper-left of this byte lane
-          for (int i = t; i < rb; i += bpp) {
-            const int b = u[i];
-            const int pred = ft == 1 ? a : ft == 3 ? (a + b) >> 1 : paeth(a, b, cc);
-            a = (uint8_t)(c[i] + pred);
-            c[i] = (uint8_t)a;
-            cc = b;
-          }
-        }
+      const uint8_t* c;
+      if (wide) {
+        png_unfilter_row(src + 1, src - rb, r > 0, ft, rb, bpp, t);
+        c = src + 1;
+      } else {
+        uint8_t* cl = rows[cur];
+        for (int i = t; i < rb; i += kPngThreads) cl[i] = src[1 + i];
+        __syncthreads();
+        png_unfilter_row(cl, rows[cur ^ 1], r > 0, ft, rb, bpp, t);
+        c = cl;
       }
       __syncthreads();
       // row -> RGB8 at output row y0 + r dy, columns x0 + px dx
@@ -222,10 +243,6 @@ bool parse_png(const uint8_t* b, size_t n, PngDesc& d, std::vector<std::pair<siz
   if (!ihdr) { err = "png: no IHDR"; return false; }
   if (!iend) { err = "png: truncated file (no IEND)"; return false; }
   if (d.ctype == 3 && d.npal == 0) { err = "png: palette image without PLTE"; return false; }
-  if (row_bytes(d.w, d.channels, d.depth) > kPngMaxRow) {
-    err = "png: rows wider than " + std::to_string(kPngMaxRow) + " bytes are not supported";
-    return false;
-  }
   return true;
 }
 
@@ -251,6 +268,27 @@ bool inflate_idat(const uint8_t* b, const std::vector<std::pair<size_t, size_t>>
     return false;
   }
   if (got != need) { err = "png: truncated image data"; return false; }
+  return true;
+}
+
+// Every row's filter-type byte is 0..4 (libpng: "bad adaptive filter value" otherwise);
+// rows = the inflated, still filtered scanlines of all passes
+bool check_filters(const PngDesc& d, const uint8_t* rows, std::string& err) {
+  int64_t pos = 0;
+  for (int p = 0; p < (d.interlace ? 7 : 1); ++p) {
+    const int x0 = d.interlace ? kA7X0h[p] : 0, y0 = d.interlace ? kA7Y0h[p] : 0;
+    const int dx = d.interlace ? kA7DXh[p] : 1, dy = d.interlace ? kA7DYh[p] : 1;
+    const int64_t pw = d.w > x0 ? (d.w - x0 + dx - 1) / dx : 0;
+    const int64_t ph = d.h > y0 ? (d.h - y0 + dy - 1) / dy : 0;
+    if (!pw || !ph) continue;
+    const int64_t rb = row_bytes((int)pw, d.channels, d.depth);
+    for (int64_t r = 0; r < ph; ++r, pos += 1 + rb)
+      if (rows[pos] > 4) {
+        err = "png: bad adaptive filter value " + std::to_string(rows[pos]) + " (pass " +
+              std::to_string(p) + ", row " + std::to_string(r) + ")";
+        return false;
+      }
+  }
   return true;
 }
 
@@ -319,6 +357,23 @@ extern "C" int vtd_png_info(const uint8_t* png, size_t len, int* h, int* w, int*
   return VTD_OK;
 }
 
+// The host half of vtd_png_decode for one file: the chunk walk, the zlib inflate of the IDAT
+// stream and the filter-byte check, into a caller host buffer (no device call)
+extern "C" int vtd_png_inflate(const uint8_t* png, size_t len, uint8_t* out, size_t out_bytes,
+                               size_t* need) {
+  VTD_CHECK_ARG(png && len > 0 && need, "png_inflate: bad arguments");
+  vtd::PngDesc d;
+  std::vector<std::pair<size_t, size_t>> idat;
+  std::string err;
+  if (!vtd::parse_png(png, len, d, &idat, err)) return vtd::fail(VTD_ERR_UNSUPPORTED, err);
+  *need = (size_t)vtd::filtered_bytes(d);
+  if (!out) return VTD_OK;
+  if (out_bytes < *need) return vtd::fail(VTD_ERR_WORKSPACE, "png_inflate: output buffer too small");
+  if (!vtd::inflate_idat(png, idat, out, *need, err) || !vtd::check_filters(d, out, err))
+    return vtd::fail(VTD_ERR_UNSUPPORTED, err);
+  return VTD_OK;
+}
+
 extern "C" int vtd_png_workspace_bytes(const uint8_t* const* pngs, const size_t* lens, int n,
                                        int32_t* dims, size_t* bytes) {
   VTD_CHECK_ARG(bytes, "png_workspace_bytes: null bytes pointer");
@@ -365,7 +420,8 @@ extern "C" int vtd_png_decode(const uint8_t* const* pngs, const size_t* lens, in
   png_parallel_for(n, [&](int i0, int i1) {
     for (int i = i0; i < i1; ++i)
       ok[i] = inflate_idat(pngs[i], idat[i], sg.host + data_off + D[i].data_off,
-                           (size_t)filtered_bytes(D[i]), errs[i]);
+                           (size_t)filtered_bytes(D[i]), errs[i]) &&
+              check_filters(D[i], sg.host + data_off + D[i].data_off, errs[i]);
   });
   for (int i = 0; i < n; ++i)
     if (!ok[i]) return fail(VTD_ERR_UNSUPPORTED, errs[i] + " (image " + std::to_string(i) + ")");
@@ -382,18 +438,22 @@ extern "C" int vtd_png_decode(const uint8_t* const* pngs, const size_t* lens, in
 }
 
 // ------------------------------------------------------------------ BMP
-// `tf.image.decode_image(file, channels=3)` on BMP files goes through TF's decode_bmp
-// (tensorflow/core/kernels/image/decode_bmp_op.cc): uncompressed rows, bottom-up unless the
-// height is negative, each row padded to 4 bytes, BGR(A) -> RGB(A), and the file's
-// bits-per-pixel / 8 must equal the requested channel count -- so with channels = 3 only
-// 24-bit files decode; the others are refused by name here as TF refuses them.  The host
-// reads the 54-byte header; the pixel array goes to the workspace in one copy and
+// `tf.image.decode_image(file, channels=3)` on BMP files: TF 2.x's decode_image is the
+// DecodeImageV2 op (tensorflow/core/kernels/image/decode_image_op.cc, DecodeBmpV2): it reads
+// bits-per-pixel (byte 28) and the pixel-array offset (byte 10), takes the file's channels =
+// bpp / 8 (1, 3 or 4; anything else is an error), row size (bpp * w + 31) / 32 * 4, bottom-up
+// rows unless the height is negative, and converts to the 3 requested channels: 8-bit -> the
+// byte replicated (the palette is NOT applied), 24-bit BGR -> RGB, 32-bit BGRA -> RGB (alpha
+// dropped).  The compression field is not read by TF; here BI_RGB (0) and BI_BITFIELDS (3)
+// files decode that way and RLE files (1, 2), whose bytes TF would misread as pixels, are
+// refused.  TF is not importable here: parity against it is unpinned (restated from that
+// source).  The host reads the header; the pixel array goes to the workspace in one copy and
 // bmp_convert_kernel (one thread per output pixel) writes the RGB8 rows.
 namespace vtd {
 namespace {
 
 struct BmpDesc {
-  int w, h, top_down, row_size;
+  int w, h, top_down, row_size, in_ch;
   int64_t data_off, out_off;
 };
 
@@ -405,11 +465,15 @@ __global__ __launch_bounds__(256) void bmp_convert_kernel(const BmpDesc* __restr
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < npx; i += (int64_t)gridDim.x * 256) {
     const int y = (int)(i / d.w), x = (int)(i - (int64_t)y * d.w);
     const int sy = d.top_down ? y : d.h - 1 - y;
-    const uint8_t* s = data + d.data_off + (int64_t)sy * d.row_size + 3 * x;
+    const uint8_t* s = data + d.data_off + (int64_t)sy * d.row_size + (int64_t)d.in_ch * x;
     uint8_t* o = out + d.out_off + 3 * i;
-    o[0] = s[2];
-    o[1] = s[1];
-    o[2] = s[0];
+    if (d.in_ch == 1) {
+      o[0] = o[1] = o[2] = s[0];
+    } else {
+      o[0] = s[2];
+      o[1] = s[1];
+      o[2] = s[0];
+    }
   }
 }
 
@@ -423,10 +487,14 @@ bool parse_bmp(const uint8_t* b, size_t n, BmpDesc& d, int64_t& pix_off, std::st
   const int32_t w = le32(b + 18), h = le32(b + 22);
   const int bpp = le16(b + 28);
   const int32_t comp = le32(b + 30);
-  if (comp != 0) { err = "bmp: compressed BMP files are not supported (TF decode_bmp reads BI_RGB rows)"; return false; }
-  if (bpp != 24) {
-    err = "bmp: " + std::to_string(bpp) + "-bit file: TF's decode_bmp needs bits-per-pixel / 8 == "
-          "the 3 requested channels";
+  if (bpp != 8 && bpp != 24 && bpp != 32) {
+    err = "bmp: " + std::to_string(bpp) + "-bit file: TF's decoder takes 8-, 24- and 32-bit "
+          "files (channels = bits-per-pixel / 8 in 1, 3, 4)";
+    return false;
+  }
+  if (comp == 1 || comp == 2) {
+    err = "bmp: RLE-compressed BMP files are not supported (TF's decoder reads every file as "
+          "uncompressed rows)";
     return false;
   }
   if (w <= 0 || h == 0 || h == INT32_MIN) { err = "bmp: bad size"; return false; }
@@ -437,7 +505,8 @@ bool parse_bmp(const uint8_t* b, size_t n, BmpDesc& d, int64_t& pix_off, std::st
   d.w = w;
   d.h = h < 0 ? -h : h;
   d.top_down = h < 0;
-  d.row_size = (int)(((int64_t)24 * w + 31) / 32 * 4);
+  d.in_ch = bpp / 8;
+  d.row_size = (int)(((int64_t)bpp * w + 31) / 32 * 4);
   if (pix_off < 54 || (uint64_t)pix_off + (uint64_t)d.row_size * d.h > n) {
     err = "bmp: truncated pixel array";
     return false;

@@ -454,15 +454,18 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
   // Launches are interleaved part by part, one stage (encoder layer) at a time: issuing
   // all of one part's ~110 launches before the next part's first one left the second
   // stream idle for the host's whole enqueue time of the first (~0.7 ms at C2, B = 256).
-  for (int t = 0; t < n_stages + stagger; ++t)
+  for (int t = 0; t < n_stages + stagger; ++t) {
+    // stagger k: the fork is recorded once part 0 has issued stages 0 .. k - 1, before it
+    // issues stage k, so the other parts run exactly k stages behind
+    if (side && stagger > 0 && t == stagger && (rc = fork())) return rc;
     for (int part = 0; part < ns; ++part) {
       Part& P = parts[part];
       const int s = part == 0 ? t : t - stagger;
-      if (part == 1 && t == stagger && stagger > 0 && (rc = fork())) return rc;
       if (s < 0 || s >= n_stages) continue;
       rc = forward_impl(&P.cfg, w, P.images, P.logits, P.dets, P.ws, P.st, s, s + 1, P.partials);
       if (rc) return rc;
     }
+  }
   if (side) {                       // join: each side stream's record and the caller's wait
     for (int part = 1; part < ns; ++part) {
       VTD_HIP(hipEventRecord(side->join[part - 1], side->s[part - 1]));
