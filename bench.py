@@ -116,6 +116,132 @@ def gemm_alg_bytes(kw, dims, b, rb=2):
     return tot / len(g)
 
 
+# ---- parity mode (north_star's tolerance on the driver's line): the committed batched golden
+# case of the headline config (tests/golden/batched_forward.json "c2_vitb16_imgs8": 8 images,
+# fp64 oracle logits, made by tests/golden/make_golden.py) placed among filler images exactly
+# as tests/test_gpu_batch_parity.py places them.  The weights and images are regenerated from
+# the fixture's seeds by the same numpy draws the golden script used (glorot / N(0, perturb)
+# in Keras weight order; U(-1, 1) images) -- tests/test_host_cpu.py checks these two functions
+# against the oracle's generators.
+GOLDEN_CASE, GOLDEN_POS = "c2_vitb16_imgs8", [0, 1, 97, 127, 128, 200, 254, 255]
+
+
+def golden_weights(weight_shapes, seed, perturb):
+    """Keras-default-like init with N(0, perturb) on biases / gamma / beta, drawn in Keras
+    weight-creation order (the golden fixture's generator)."""
+    import math
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    out = {}
+    for name, shape in weight_shapes.items():
+        shape = tuple(shape)
+        if name.endswith("/embeddings"):
+            v = rng.uniform(-0.05, 0.05, size=shape)
+        elif name.endswith("/kernel"):
+            if len(shape) == 2:
+                fi, fo = shape
+            else:
+                rf = int(np.prod(shape[:-2]))
+                fi, fo = shape[-2] * rf, shape[-1] * rf
+            lim = math.sqrt(6.0 / (fi + fo))
+            v = rng.uniform(-lim, lim, size=shape)
+        elif name.endswith("/gamma"):
+            v = np.ones(shape) + (rng.normal(0, perturb, size=shape) if perturb else 0)
+        else:
+            v = rng.normal(0, perturb, size=shape) if perturb else np.zeros(shape)
+        out[name] = v.astype(np.float32)
+    return out
+
+
+def golden_images(n, shape, seed, letterbox):
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    h, w, c = shape
+    img = rng.uniform(-1.0, 1.0, size=(n, h, w, c)).astype(np.float32)
+    if letterbox:
+        band = h // 8
+        img[:, :band] = -1.0
+        img[:, h - band:] = -1.0
+    return img
+
+
+def parity_mode(args, dev, kw_run):
+    """North_star's fp32 tolerance on the headline workload, timed like the headline: the fp32
+    parity mode and the split-bf16 mode (bf16x3) at C2 B = 256, W warm-up + K timed steps
+    (forward + fused decode, two streams), the GEMM class's fraction of the fp32 peak from a
+    one-stream profiled pass, and the max relative error of the 8 golden rows against their
+    fp64 oracle logits ("rel": max |y - ref| / max |ref| per image; "within_1e-3": the
+    |y - ref| <= 1e-3 |ref| + 1e-3 max|ref| test of tests/test_gpu_batch_parity.py) -- checked
+    outside the timed region."""
+    import ctypes
+    import hashlib
+    import numpy as np
+    import vision_transformer_detector_amd as vtd
+    from vision_transformer_detector_amd import _lib as L
+    spec = json.load(open(os.path.join(ROOT, "tests", "golden", "batched_forward.json")))[GOLDEN_CASE]
+    kw = dict(spec["kwargs"])
+    kw["input_shape"] = tuple(kw["input_shape"])
+    probe = vtd.create_vision_transformer_detector(**kw, dtype="float32", device=dev, seed=0)
+    shape = probe.input_shape
+    imgs = golden_images(spec["n"], shape, spec["image_seed"], spec["letterbox"])
+    if hashlib.sha256(np.ascontiguousarray(imgs).tobytes()).hexdigest() != spec["images_sha256"]:
+        return {"error": "golden images do not regenerate from their seed"}
+    w = golden_weights(probe.weight_shapes, spec["weight_seed"], spec["perturb"])
+    del probe
+    B = 256
+    gen = torch.Generator(device=dev).manual_seed(77)
+    x = torch.rand((B,) + tuple(shape), generator=gen, device=dev) * 2 - 1
+    for i, p in enumerate(GOLDEN_POS):
+        x[p] = torch.from_numpy(imgs[i]).to(dev)
+    ref = [np.asarray(r, np.float64) for r in spec["logits"]]
+    out = {"workload": f"{GOLDEN_CASE}: ViT-B/16 @224 (the headline preset), batch {B}, "
+                       f"golden rows at {GOLDEN_POS}", "steps": args.steps, "warmup": args.warmup}
+    for mode in ("float32", "bf16x3"):
+        model = vtd.create_vision_transformer_detector(**kw, dtype=mode, device=dev, seed=0)
+        model.set_weights(w)
+        for _ in range(args.warmup):
+            model.detect(x)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            model.detect(x)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        logits, _ = model.detect(x)
+        y = logits.cpu().numpy().astype(np.float64)
+        rel, ok = 0.0, True
+        for i, p in enumerate(GOLDEN_POS):
+            err = np.abs(y[p] - ref[i])
+            rel = max(rel, float(err.max() / np.abs(ref[i]).max()))
+            ok = ok and bool(np.all(err <= 1e-3 * np.abs(ref[i]) + 1e-3 * np.abs(ref[i]).max()))
+        # the GEMM class alone (one stream, hipEvents around every launch)
+        L.check(L.lib.vtd_profile_reset())
+        L.check(L.lib.vtd_profile_enable(1))
+        for _ in range(max(1, args.steps // 4)):
+            model.detect(x)
+        torch.cuda.synchronize()
+        L.check(L.lib.vtd_profile_enable(0))
+        ms = (ctypes.c_double * L.PROF_CLASSES)()
+        nl = (ctypes.c_int64 * L.PROF_CLASSES)()
+        fl = (ctypes.c_double * L.PROF_CLASSES)()
+        L.check(L.lib.vtd_profile_read(ms, nl, fl, L.PROF_CLASSES))
+        gemm_tf = fl[0] / (ms[0] * 1e-3) / 1e12 if ms[0] > 0 else None
+        rec = {"value": round(B * args.steps / el, 2), "unit": "images/s",
+               "ms_per_step": round(1e3 * el / args.steps, 3),
+               "max_rel_err_golden_rows": float(f"{rel:.3e}"), "within_1e-3": ok,
+               "gemm_tflops": round(gemm_tf, 1) if gemm_tf else None,
+               "gemm_frac_of_fp32_peak": round(gemm_tf / PEAK_TFLOPS["f32"], 4) if gemm_tf else None}
+        if mode == "bf16x3" and gemm_tf:
+            # three bf16 MFMA products per algorithmic one: the matrix cores' own load
+            rec["gemm_mfma_frac_of_bf16_peak"] = round(3 * gemm_tf / PEAK_TFLOPS["bf16"], 4)
+        out[mode] = rec
+        del model
+        torch.cuda.empty_cache()
+    if out.get("float32", {}).get("value"):
+        out["bf16x3_over_float32"] = round(out["bf16x3"]["value"] / out["float32"]["value"], 3)
+    return out
+
+
 def cpu_baseline(model, kw, shape, preset):
     """The oracle's fp32 torch-CPU restatement (oracle/vtd_torch_cpu.py) of the same graph on
     the host cores: the reference's TF-CPU path cannot run in this pipeline (TF/Keras/tfa
@@ -289,6 +415,8 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32", "fp8"])
     ap.add_argument("--preset", default="vit_b16_224")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity-mode", action="store_true",
+                    help="skip the f32 / split-bf16 parity-mode sub-record (headline config only)")
     ap.add_argument("--streams", type=int, default=2,
                     help="vtd_forward micro-batch streams (VTD_STREAMS; 1 = one stream)")
     ap.add_argument("--graph", type=int, default=0,
@@ -464,6 +592,8 @@ def main():
         "rank_ms_min": round(1e3 * spread["min_s"] / args.steps, 3),
         "rank_ms_max": round(1e3 * spread["max_s"] / args.steps, 3),
     }
+    if world == 1 and headline and not args.no_parity_mode:
+        out["parity_mode"] = parity_mode(args, dev, kw)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(model, kw, shape, args.preset)
     if rank == 0:

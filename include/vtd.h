@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define VTD_ABI_VERSION 14
+#define VTD_ABI_VERSION 15
 #define VTD_KALIGN 64          /* K / row padding granule, elements              */
 #define VTD_MAX_MLP 16         /* max encoder_mlp_quantities                     */
 #define VTD_MAX_HEAD 64        /* max mlp_head layers * repeats                   */
@@ -45,10 +45,25 @@ typedef enum vtd_status {
 typedef enum vtd_dtype {       /* compute (GEMM operand) dtype                   */
   VTD_F32 = 0,                 /* parity mode: f32 operands, f32 MFMA            */
   VTD_BF16 = 1,                /* throughput mode: bf16 operands, f32 accumulate */
-  VTD_FP8 = 2                  /* forward mode only (vtd_config.dtype): encoder  */
+  VTD_FP8 = 2,                 /* forward mode only (vtd_config.dtype): encoder  */
                                /* Dense layers in MX-fp8 (vtd_gemm_mx8), the rest */
                                /* as VTD_BF16                                     */
+  VTD_BF16X3 = 3               /* split-bf16 parity mode: every Dense layer as    */
+                               /* three bf16 MFMA products with f32 accumulation, */
+                               /* the rest fp32 (see "Split-bf16 operands")       */
 } vtd_dtype;
+
+/* Split-bf16 operands (VTD_BF16X3).  An f32 value v is held as hi = bf16(v) (round to
+ * nearest even) and lo = bf16(v - hi): hi + lo carries 16 significand bits, and
+ * hi_a hi_b + lo_a hi_b + hi_a lo_b leaves out only lo_a lo_b (<= 2^-18 |a b|).  A K-wide
+ * f32 row is stored as a bf16 row of THREE P-wide pieces (P = row stride / 3 >= K, the
+ * columns [K, P) of every piece zero):
+ *   A operand (activations, role 0):  [ hi | lo | hi ]
+ *   B operand (weights W^T, role 1):  [ hi | hi | lo ]
+ * so one ordinary bf16 GEMM over K' = 3 P (vtd_gemm, dtype VTD_BF16, lda = ldb = 3 P) sums
+ * the three products in its fp32 accumulators.  Producers write the A form directly:
+ * vtd_epilogue.out_dtype = VTD_BF16X3, vtd_layernorm / vtd_extract_patches with
+ * dtype = VTD_BF16X3 (ldo / ldy = 3 P); vtd_split_bf16x3 converts any f32 matrix. */
 
 typedef enum vtd_act {         /* activation fused in a GEMM epilogue            */
   VTD_ACT_NONE = 0,
@@ -149,10 +164,17 @@ int vtd_pack_dense(const float* src_dev, int K, int N, int k_group, int k_group_
 int vtd_pack_vector(const float* src_dev, int N, int n_group, int n_group_p,
                     float* dst_dev, int offset, void* stream);
 
+/* f32 x [rows][ldx] (first K columns) -> split-bf16 y [rows][ldy] (three P = ldy / 3 wide
+ * pieces, P >= K; role 0: [hi | lo | hi], role 1: [hi | hi | lo]; columns [K, P) of each
+ * piece written as zero).  ldy % 3 == 0. */
+int vtd_split_bf16x3(const float* x_dev, int64_t rows, int K, int ldx, void* y_dev, int ldy,
+                     int role, void* stream);
+
 /* ---------------------------------------------------------------- per-op ------- */
 /* ExtractImagePatches (vtd.py:177-206) + Reshape flatten_patches (vtd.py:279-280):
  * images NHWC fp32 [B][H][W][C] -> patches [B*N][ld_out] (dtype), SAME zero pad,
- * (kh, kw, c) order; columns [P, ld_out) written as zero. */
+ * (kh, kw, c) order; columns [P, ld_out) written as zero.  dtype VTD_BF16X3: the split-bf16
+ * A operand, three ld_out / 3 wide pieces. */
 int vtd_extract_patches(const float* images_dev, int B, int H, int W, int C, int p,
                         void* out_dev, int ld_out, int dtype, void* stream);
 
@@ -160,7 +182,9 @@ int vtd_extract_patches(const float* images_dev, int B, int H, int W, int C, int
  * C[m][n] = act(sum_k A[m][k] * Bt[n][k] + bias[n] + rowadd[m % rowadd_period]
  *               (rowadd only for n < rowadd_ncols)) + resid[m][n]
  * for m < M, n < N.  A, Bt in `dtype`; K % VTD_KALIGN == 0; lda, ldb % 8 == 0.
- * out: fp32 (out_dtype 0) or bf16 (1); out2 (nullable) a second bf16 copy.
+ * out: fp32 (out_dtype 0), bf16 (1) or split-bf16 (VTD_BF16X3: the next GEMM's A operand
+ * [hi | lo | hi], three ldo / 3 wide pieces, ldo % 3 == 0, ldo / 3 >= N; dtype VTD_BF16
+ * only); out2 (nullable) a second bf16 copy.
  * scatter_tokens > 0 selects the head Reshape epilogue (vtd.py:461-463): element
  * (m = b*T + t, n < 17) is stored at out[(b*17 + f / T) * ldo + f % T], f = t*17 + n. */
 typedef struct vtd_epilogue {
@@ -230,7 +254,8 @@ int vtd_gemm_mx8(int M, int N, int K, const uint8_t* A_dev, int lda, const uint8
 
 /* keras LayerNormalization(axis=-1, epsilon) (vtd.py:353-357, 375-379):
  * x (x_dtype: fp32, or the bf16 residual stream) [rows][ldx] -> y (dtype) [rows][ldy];
- * fp32 statistics over the first D columns; columns [D, ldy) of y written as zero. */
+ * fp32 statistics over the first D columns; columns [D, ldy) of y written as zero.
+ * dtype VTD_BF16X3: y is the split-bf16 A operand, three ldy / 3 wide pieces. */
 int vtd_layernorm(const void* x_dev, int x_dtype, int64_t rows, int D, int ldx,
                   const float* gamma_dev, const float* beta_dev, float eps,
                   void* y_dev, int ldy, int dtype, void* stream);

@@ -1,0 +1,215 @@
+"""Split-bf16 parity mode (dtype VTD_BF16X3 / "bf16x3"; include/vtd.h "Split-bf16 operands").
+
+An f32 value v is held as hi = bf16(v) (round to nearest even) and lo = bf16(v - hi); a Dense
+layer runs as ONE bf16 MFMA GEMM over K' = 3 K on the rows [hi | lo | hi] (activations, A) and
+[hi | hi | lo] (weights, B), i.e. hi.hi + lo.hi + hi.lo summed in fp32 accumulators.  Checks:
+  * the split itself is bit-exact against a numpy restatement (split_np below);
+  * every producer that writes the split operand directly -- the GEMM epilogues (generic,
+    LDS-staged fast, register-direct transposed; the head's Reshape scatter; split-K), the
+    LayerNorm kernels, patch extraction -- writes exactly split_np of its f32 result;
+  * a split-bf16 GEMM is within 2e-5 of the fp64 product of the f32 operands (the dropped
+    lo.lo term is <= 2^-18 of each product).
+The whole-forward goldens for this mode are in test_gpu_model.py / test_gpu_batch_parity.py
+(tolerance 1e-4)."""
+import ctypes
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import vtd_numpy as ref
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def L(cuda):
+    from vision_transformer_detector_amd import _lib
+    return _lib
+
+
+def bf16_rne(x):
+    """f32 -> bf16 bits (uint16) by round to nearest even (finite inputs)."""
+    u = np.ascontiguousarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+
+
+def bf16_to_f32(b):
+    return (b.astype(np.uint32) << 16).view(np.float32)
+
+
+def split_np(x, P, role):
+    """f32 [rows][K] -> uint16 [rows][3P]: role 0 [hi | lo | hi], role 1 [hi | hi | lo]."""
+    x = np.asarray(x, np.float32)
+    rows, K = x.shape
+    xp = np.zeros((rows, P), np.float32)
+    xp[:, :K] = x
+    hi = bf16_rne(xp)
+    lo = bf16_rne(xp - bf16_to_f32(hi))
+    return np.concatenate([hi, lo, hi] if role == 0 else [hi, hi, lo], axis=1)
+
+
+def as_u16(t):
+    return t.cpu().view(torch.int16).numpy().view(np.uint16)
+
+
+def split_dev(L, x, P, role):
+    rows, K = x.shape
+    y = torch.full((rows, 3 * P), -1, dtype=torch.int16, device=x.device)
+    L.check(L.lib.vtd_split_bf16x3(x.data_ptr(), rows, K, x.shape[1], y.data_ptr(), 3 * P, role,
+                                   L.stream_ptr()), "split")
+    torch.cuda.synchronize()
+    return y.view(torch.bfloat16)
+
+
+@pytest.mark.parametrize("rows,K,P", [(5, 64, 64), (33, 100, 128), (7, 13, 24), (256, 768, 768)])
+@pytest.mark.parametrize("role", [0, 1])
+def test_split_bit_exact(L, cuda, rows, K, P, role):
+    g = torch.Generator().manual_seed(rows + K + role)
+    x = torch.randn(rows, K, generator=g) * torch.logspace(-6, 6, K)    # wide exponent range
+    x[0, :min(K, 4)] = torch.tensor([0.0, -0.0, 1e-30, -3.0e38])[:min(K, 4)]
+    y = split_dev(L, x.to(cuda), P, role)
+    assert np.array_equal(as_u16(y), split_np(x.numpy(), P, role))
+
+
+def _epi(L, out, ldo, out_dtype, bias=None, act=0, scatter=0, resid=None):
+    e = L.VtdEpilogue()
+    e.bias, e.act = L.ptr(bias), act
+    e.out, e.ldo, e.out_dtype = L.ptr(out), ldo, out_dtype
+    e.scatter_tokens = scatter
+    e.resid = L.ptr(resid)
+    e.ldr = resid.shape[1] if resid is not None else 0
+    return e
+
+
+def _gemm_x3(L, A32, W32, N=None, **kw):
+    """split-bf16 GEMM of f32 operands A [M][K], W^T [N][K] (K % 64 == 0)."""
+    M, K = A32.shape
+    a3 = split_dev(L, A32, K, 0)
+    b3 = split_dev(L, W32, K, 1)
+    return a3, b3
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 64, 64), (300, 200, 192), (1024, 768, 768),
+                                   (8192, 1024, 256), (512, 17, 256)])
+def test_split_gemm_vs_fp64(L, cuda, M, N, K):
+    """A split-bf16 GEMM (bf16 kernels over K' = 3K: the 256-tile pp2 kernel for the larger
+    shapes, the 128-tile / skinny kernels for the small ones) against the fp64 product of the
+    f32 operands."""
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) / math.sqrt(K)
+    a3, b3 = _gemm_x3(L, A.to(cuda), W.to(cuda))
+    out = torch.full((M, N), float("nan"), device=cuda)
+    e = _epi(L, out, N, L.F32)
+    L.check(L.lib.vtd_gemm(M, N, 3 * K, a3.data_ptr(), 3 * K, b3.data_ptr(), 3 * K, L.BF16,
+                           ctypes.byref(e), L.stream_ptr()), "gemm")
+    torch.cuda.synchronize()
+    ref64 = A.double() @ W.double().T
+    err = (out.cpu().double() - ref64).abs().max().item()
+    assert err <= 2e-5 * ref64.abs().max().item(), err
+
+
+@pytest.mark.parametrize("M,N,K,act", [(8192, 1024, 256, 0), (4096, 3072, 256, 1),
+                                       (8000, 1024, 256, 2), (512, 1536, 256, 2),
+                                       (300, 200, 192, 1), (64, 6, 128, 0),
+                                       (4352, 1088, 2176, 1)])
+def test_split_output_equals_split_of_f32_output(L, cuda, M, N, K, act):
+    """out_dtype VTD_BF16X3 (EPI_S3 on the fast pp2 epilogues, the generic epilogue on partial
+    tiles and small problems, split-K for the head's few-tile long-K shape) writes exactly
+    split_np of the same GEMM's f32 output (same accumulators, same bias / activation)."""
+    g = torch.Generator().manual_seed(N + act)
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16).to(cuda)
+    W = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(torch.bfloat16).to(cuda)
+    bias = torch.randn(N, generator=g).to(cuda)
+    f32 = torch.empty(M, N, device=cuda)
+    P = ((N + 63) // 64) * 64
+    s3 = torch.full((M, 3 * P), -1, dtype=torch.int16, device=cuda)
+    for out, ldo, od in ((f32, N, L.F32), (s3, 3 * P, L.BF16X3)):
+        e = _epi(L, out, ldo, od, bias=bias, act=act)
+        ks = L.lib.vtd_gemm_splitk_choice(M, N, K, L.BF16)
+        if ks > 1:
+            part = torch.empty(ks * M * N, device=cuda)
+            L.check(L.lib.vtd_gemm_splitk(M, N, K, A.data_ptr(), K, W.data_ptr(), K,
+                                          ctypes.byref(e), part.data_ptr(), part.numel() * 4, ks,
+                                          L.stream_ptr()), "splitk")
+        else:
+            L.check(L.lib.vtd_gemm(M, N, K, A.data_ptr(), K, W.data_ptr(), K, L.BF16,
+                                   ctypes.byref(e), L.stream_ptr()), "gemm")
+    torch.cuda.synchronize()
+    want = split_np(f32.cpu().numpy(), P, 0)
+    got = as_u16(s3)
+    for piece in range(3):                     # columns [N, P) of each piece are not written
+        sl = slice(piece * P, piece * P + N)
+        assert np.array_equal(got[:, sl], want[:, sl]), piece
+
+
+def test_split_scatter_epilogue(L, cuda):
+    """The head's Dense(17) + Reshape scatter (vtd.py:454-463) with a split-bf16 output."""
+    B, T, K = 3, 196, 768
+    g = torch.Generator().manual_seed(17)
+    A = torch.randn(B * T, K, generator=g).to(torch.bfloat16).to(cuda)
+    W = (torch.randn(17, K, generator=g) / math.sqrt(K)).to(torch.bfloat16).to(cuda)
+    bias = torch.randn(17, generator=g).to(cuda)
+    P = 256
+    f32 = torch.zeros(B * 17, P, device=cuda)
+    s3 = torch.zeros(B * 17, 3 * P, dtype=torch.int16, device=cuda)
+    for out, ldo, od in ((f32, P, L.F32), (s3, 3 * P, L.BF16X3)):
+        e = _epi(L, out, ldo, od, bias=bias, scatter=T)
+        L.check(L.lib.vtd_gemm(B * T, 17, K, A.data_ptr(), K, W.data_ptr(), K, L.BF16,
+                               ctypes.byref(e), L.stream_ptr()), "gemm")
+    torch.cuda.synchronize()
+    assert np.array_equal(as_u16(s3), split_np(f32.cpu().numpy(), P, 0))
+
+
+@pytest.mark.parametrize("rows,D,P", [(300, 768, 768), (77, 28, 64), (64, 1024, 1024),
+                                      (9, 100, 128), (9, 30, 64)])
+@pytest.mark.parametrize("xdt", ["f32", "bf16"])
+def test_layernorm_split_output(L, cuda, rows, D, P, xdt):
+    """vtd_layernorm with dtype VTD_BF16X3 = split_np of its f32 output (the 16-column, the
+    4-column and the generic kernels)."""
+    g = torch.Generator().manual_seed(rows + D)
+    x = (torch.randn(rows, P, generator=g) * 3 + 1)
+    x[:, D:] = 0
+    tdt, code = (torch.float32, L.F32) if xdt == "f32" else (torch.bfloat16, L.BF16)
+    x = x.to(tdt).to(cuda)
+    gamma = (1 + 0.1 * torch.randn(P, generator=g)).to(cuda)
+    beta = (0.1 * torch.randn(P, generator=g)).to(cuda)
+    f32 = torch.empty(rows, P, device=cuda)
+    s3 = torch.full((rows, 3 * P), -1, dtype=torch.int16, device=cuda)
+    for out, ldy, od in ((f32, P, L.F32), (s3, 3 * P, L.BF16X3)):
+        L.check(L.lib.vtd_layernorm(x.data_ptr(), code, rows, D, P, gamma.data_ptr(),
+                                    beta.data_ptr(), 1e-3, out.data_ptr(), ldy, od,
+                                    L.stream_ptr()), "layernorm")
+    torch.cuda.synchronize()
+    assert np.array_equal(as_u16(s3), split_np(f32.cpu().numpy(), P, 0))
+
+
+@pytest.mark.parametrize("H,W,p,P", [(224, 224, 16, 768), (40, 36, 8, 192), (608, 608, 17, 896)])
+def test_patches_split_output(L, cuda, H, W, p, P):
+    g = torch.Generator().manual_seed(H + p)
+    img = (torch.rand(2, H, W, 3, generator=g) * 2 - 1).to(cuda)
+    gh, gw = -(-H // p), -(-W // p)
+    rows = 2 * gh * gw
+    f32 = torch.empty(rows, P, device=cuda)
+    s3 = torch.full((rows, 3 * P), -1, dtype=torch.int16, device=cuda)
+    for out, ldo, od in ((f32, P, L.F32), (s3, 3 * P, L.BF16X3)):
+        L.check(L.lib.vtd_extract_patches(img.data_ptr(), 2, H, W, 3, p, out.data_ptr(), ldo, od,
+                                          L.stream_ptr()), "patches")
+    torch.cuda.synchronize()
+    assert np.array_equal(as_u16(s3), split_np(f32.cpu().numpy(), P, 0))
+    want = ref.extract_patches_same(img.cpu().numpy().astype(np.float64), p).reshape(rows, -1)
+    assert np.array_equal(f32.cpu().numpy()[:, :want.shape[1]], want.astype(np.float32))
+
+
+def test_split_arguments_validated(L, cuda):
+    x = torch.zeros(4, 64, device=cuda)
+    y = torch.zeros(4, 190, dtype=torch.int16, device=cuda)
+    assert L.lib.vtd_split_bf16x3(x.data_ptr(), 4, 64, 64, y.data_ptr(), 190, 0, None) == -1
+    assert L.lib.vtd_split_bf16x3(x.data_ptr(), 4, 64, 64, y.data_ptr(), 180, 0, None) == -1
+    assert L.lib.vtd_split_bf16x3(x.data_ptr(), 4, 64, 64, y.data_ptr(), 192, 2, None) == -1
+    out = torch.zeros(4, 190, dtype=torch.int16, device=cuda)
+    e = _epi(L, out, 190, L.BF16X3)
+    assert L.lib.vtd_gemm(4, 64, 64, x.data_ptr(), 64, x.data_ptr(), 64, L.F32, ctypes.byref(e),
+                          None) == -1            # split output needs bf16 operands

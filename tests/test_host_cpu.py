@@ -228,3 +228,33 @@ def test_gemm_lds_swizzle_conflict_free():
     r = subprocess.run([sys.executable, os.path.join(root, "tools", "swizzle_check.py")],
                        capture_output=True, text=True)
     assert r.returncode == 0 and "conflict-free" in r.stdout
+
+
+def test_bench_golden_generators_match_oracle():
+    """bench.py's parity_mode regenerates the batched golden case's weights and images without
+    the oracle (golden_weights / golden_images); they must be the oracle's draws exactly."""
+    import json
+    import bench
+    from oracle import vtd_numpy as V
+    from vision_transformer_detector_amd.detector import keras_weight_names
+    from vision_transformer_detector_amd import _lib as L2
+    kw = dict(input_shape=(40, 36, 3), patch_size=8, embedding_dim=24, encoder_num_heads=3,
+              encoder_key_dim=10, encoder_mlp_quantities=3, encoder_repeat_times=2,
+              mlp_head_last_units=8, mlp_head_dense_layers_quantity=3)
+    full = V.resolve_kwargs(**kw)
+    cfg = L2.VtdConfig(batch=1, image_h=40, image_w=36, channels=3, patch_size=8,
+                       embedding_dim=24, num_heads=3, key_dim=10, mlp_quantities=3,
+                       repeat_times=2, head_last_units=8, head_layers=3, head_repeats=1,
+                       use_mish=1, dtype=0)
+    dims = L2.VtdDims()
+    assert L2.lib.vtd_derive_dims(ctypes.byref(cfg), ctypes.byref(dims)) == 0
+    names = keras_weight_names(full, dims)
+    got = bench.golden_weights(names, seed=5, perturb=0.02)
+    want = V.init_weights(seed=5, perturb=0.02, **kw)
+    assert list(got) == list(want)
+    for n in want:
+        assert np.array_equal(got[n], want[n]), n
+    assert np.array_equal(bench.golden_images(3, (40, 36, 3), 4, True),
+                          V.synthetic_images(3, (40, 36, 3), seed=4, letterbox=True))
+    spec = json.load(open(os.path.join(ROOT, "tests", "golden", "batched_forward.json")))
+    assert bench.GOLDEN_CASE in spec and len(bench.GOLDEN_POS) == spec[bench.GOLDEN_CASE]["n"]

@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must precede loading libvtd.so, see module doc)
 LIB_PATH = os.environ.get("VTD_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                           "libvtd.so")
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 KALIGN = 64
 MAX_MLP = 16
 MAX_HEAD = 64
@@ -24,7 +24,7 @@ MAX_DETECT = 17
 PROF_CLASSES = 5
 MAP_CLASSES, MAP_LATEST, MAP_PER_IMAGE, MAP_MAX_BOXES = 80, 3, 14, 64
 
-F32, BF16, FP8 = 0, 1, 2
+F32, BF16, FP8, BF16X3 = 0, 1, 2, 3
 # run-time A/B knobs (vtd_set_knob; -1 = the library default)
 KNOB_ATTN_VARIANT, KNOB_ATTN_GRID, KNOB_GEMM_NGW, KNOB_SPLITK, KNOB_JPEG_CHUNK_BITS = 0, 1, 2, 3, 4
 KNOB_SKINNY, KNOB_F32_PP2, KNOB_STAGGER, KNOB_GEMM_TR, KNOB_FIN_WGS = 5, 6, 7, 8, 9
@@ -117,6 +117,8 @@ SIGNATURES = {
                               c_void_p, c_int, c_int, c_void_p]),
     "vtd_attention_mx8": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p,
                                   c_int, c_void_p, c_int64, c_void_p]),
+    "vtd_split_bf16x3": (c_int, [c_void_p, c_int64, c_int, c_int, c_void_p, c_int, c_int,
+                                 c_void_p]),
     "vtd_decode": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "vtd_decode_detections": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                       c_float, c_float, c_void_p]),

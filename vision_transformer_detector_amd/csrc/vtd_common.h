@@ -81,6 +81,15 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2_hw));
 }
 
+// split-bf16 (VTD_BF16X3, include/vtd.h "Split-bf16 operands"): hi = bf16(v) (RNE), lo =
+// bf16(v - hi) -- v - hi is exact in f32.  For a pair packed as hi = pack_bf16x2(a, b):
+__device__ __forceinline__ uint32_t pack_lo_bf16x2(float a, float b, uint32_t hi) {
+  return pack_bf16x2(a - __uint_as_float(hi << 16), b - __uint_as_float(hi & 0xffff0000u));
+}
+__device__ __forceinline__ bf16_t lo_bf16(float v, bf16_t hi) {
+  return f32_to_bf16(v - __uint_as_float((uint32_t)hi << 16));
+}
+
 template <typename T> struct DT;
 template <> struct DT<float> {
   static constexpr int code = VTD_F32;

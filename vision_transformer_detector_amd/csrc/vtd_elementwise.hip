@@ -22,12 +22,40 @@ __device__ __forceinline__ void st4(bf16_t* p, f32x4 v) {
   *reinterpret_cast<uint2*>(p) = uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
 }
 
+// split-bf16 output (VTD_BF16X3 A operand): [hi | lo | hi] at p, p + P, p + 2 P
+__device__ __forceinline__ void st4x3(bf16_t* p, int P, f32x4 v) {
+  const uint32_t h0 = pack_bf16x2(v[0], v[1]), h1 = pack_bf16x2(v[2], v[3]);
+  const uint2 hi = {h0, h1}, lo = {pack_lo_bf16x2(v[0], v[1], h0), pack_lo_bf16x2(v[2], v[3], h1)};
+  *reinterpret_cast<uint2*>(p) = hi;
+  *reinterpret_cast<uint2*>(p + P) = lo;
+  *reinterpret_cast<uint2*>(p + 2 * P) = hi;
+}
+// one element of a row of width ldy: plain, or split over three ldy / 3 wide pieces (X3)
+template <bool X3, typename TO>
+__device__ __forceinline__ void st1(TO* yr, int c, int P, float v) {
+  if constexpr (X3) {
+    const bf16_t h = f32_to_bf16(v);
+    yr[c] = h;
+    yr[P + c] = lo_bf16(v, h);
+    yr[2 * P + c] = h;
+  } else {
+    yr[c] = DT<TO>::from(v);
+  }
+}
+template <bool X3, typename TO>
+__device__ __forceinline__ void st4v(TO* p, int P, f32x4 v) {
+  if constexpr (X3) st4x3(p, P, v);
+  else st4(p, v);
+}
+
 // TI: the residual stream's dtype (f32, or bf16 in the bf16 / fp8 modes); TO: output.
-template <typename TI, typename TO, int NV>
+// X3: TO = bf16_t and the output is the split-bf16 operand, three ldy / 3 wide pieces.
+template <typename TI, typename TO, int NV, bool X3 = false>
 __global__ __launch_bounds__(256) void layernorm_kernel(
     const TI* __restrict__ x, int64_t rows, int D, int ldx,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
     TO* __restrict__ y, int ldy) {
+  const int P = X3 ? ldy / 3 : ldy;
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -65,18 +93,19 @@ __global__ __launch_bounds__(256) void layernorm_kernel(
       f32x4 o;
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = (v[i][j] - mean) * rstd * g[j] + bb[j];
-      st4(yr + c, o);
+      st4v<X3>(yr + c, P, o);
     }
   }
-  for (int c = D + lane; c < ldy; c += 64) yr[c] = DT<TO>::from(0.f);
+  for (int c = D + lane; c < P; c += 64) st1<X3>(yr, c, P, 0.f);
 }
 
 // generic fallback (unaligned, D % 4 != 0 or D > 4096): three passes over the row
-template <typename TI, typename TO>
+template <typename TI, typename TO, bool X3 = false>
 __global__ __launch_bounds__(256) void layernorm_generic_kernel(
     const TI* __restrict__ x, int64_t rows, int D, int ldx,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
     TO* __restrict__ y, int ldy) {
+  const int P = X3 ? ldy / 3 : ldy;
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -93,8 +122,8 @@ __global__ __launch_bounds__(256) void layernorm_generic_kernel(
   q = wave_sum(q);
   const float rstd = 1.f / sqrtf(q / D + eps);
   TO* yr = y + row * ldy;
-  for (int c = lane; c < ldy; c += 64)
-    yr[c] = DT<TO>::from(c < D ? (DT<TI>::load(xr + c) - mean) * rstd * gamma[c] + beta[c] : 0.f);
+  for (int c = lane; c < P; c += 64)
+    st1<X3>(yr, c, P, c < D ? (DT<TI>::load(xr + c) - mean) * rstd * gamma[c] + beta[c] : 0.f);
 }
 
 // ---- 16 columns per lane (D % 16 == 0): the wide LayerNorm pair.  layernorm16_kernel and
@@ -173,10 +202,11 @@ __device__ __forceinline__ void ln16_out(const Ln16Row<NC>& r, int i, int c, flo
   }
 }
 
-template <typename TI, typename TO, int NC, int RPW>
+template <typename TI, typename TO, int NC, int RPW, bool X3 = false>
 __global__ __launch_bounds__(256) void layernorm16_kernel(
     const TI* __restrict__ x, int64_t rows, int D, int ldx, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, TO* __restrict__ y, int ldy) {
+  const int P = X3 ? ldy / 3 : ldy;
   const int lane = threadIdx.x & 63;
   const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
   if (row0 >= rows) return;
@@ -197,10 +227,10 @@ __global__ __launch_bounds__(256) void layernorm16_kernel(
         f32x4 o[4];
         ln16_out<NC, false>(r[k], i, c, mean, rstd, gamma, beta, o);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) st4(yr + c + 4 * g, o[g]);
+        for (int g = 0; g < 4; ++g) st4v<X3>(yr + c + 4 * g, P, o[g]);
       }
     }
-    for (int c = D + lane; c < ldy; c += 64) yr[c] = DT<TO>::from(0.f);
+    for (int c = D + lane; c < P; c += 64) st1<X3>(yr, c, P, 0.f);
   }
 }
 
@@ -259,13 +289,13 @@ bool ln16_ok(const void* x, int x_dtype, int D, int ldx, const float* g, const f
          al16(g) && al16(b);
 }
 
-template <typename TI, typename TO>
+template <typename TI, typename TO, bool X3 = false>
 int ln_dispatch(const void* xv, int64_t rows, int D, int ldx, const float* g,
                 const float* b, float eps, void* y, int ldy, hipStream_t st) {
   const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   const TI* x = static_cast<const TI*>(xv);
   TO* yo = static_cast<TO*>(y);
-  const bool vec = (D % 4 == 0) && (ldx % 4 == 0) && (ldy % 4 == 0) &&
+  const bool vec = (D % 4 == 0) && (ldx % 4 == 0) && ((X3 ? ldy / 3 : ldy) % 4 == 0) &&
                    (reinterpret_cast<uintptr_t>(x) % (4 * sizeof(TI)) == 0) &&
                    (reinterpret_cast<uintptr_t>(y) % (4 * sizeof(TO)) == 0) &&
                    (reinterpret_cast<uintptr_t>(g) % 16 == 0) &&
@@ -274,7 +304,7 @@ int ln_dispatch(const void* xv, int64_t rows, int D, int ldx, const float* g,
     constexpr int RPW = 2;
     const dim3 g16((unsigned)((rows + 4 * RPW - 1) / (4 * RPW)));
     const int nc = (D + 1023) / 1024;
-#define VTD_LN16(NC) hipLaunchKernelGGL((layernorm16_kernel<TI, TO, NC, RPW>), g16, block, 0, st, x, \
+#define VTD_LN16(NC) hipLaunchKernelGGL((layernorm16_kernel<TI, TO, NC, RPW, X3>), g16, block, 0, st, x, \
                                         rows, D, ldx, g, b, eps, yo, ldy)
     if (nc <= 1) VTD_LN16(1);
     else if (nc <= 2) VTD_LN16(2);
@@ -284,7 +314,7 @@ int ln_dispatch(const void* xv, int64_t rows, int D, int ldx, const float* g,
     return VTD_OK;
   }
   const int nv = (D + 255) / 256;
-#define VTD_LN(NV) hipLaunchKernelGGL((layernorm_kernel<TI, TO, NV>), grid, block, 0, st, x, rows, \
+#define VTD_LN(NV) hipLaunchKernelGGL((layernorm_kernel<TI, TO, NV, X3>), grid, block, 0, st, x, rows, \
                                       D, ldx, g, b, eps, yo, ldy)
   if (vec && nv <= 1) VTD_LN(1);
   else if (vec && nv <= 2) VTD_LN(2);
@@ -293,8 +323,8 @@ int ln_dispatch(const void* xv, int64_t rows, int D, int ldx, const float* g,
   else if (vec && nv <= 8) VTD_LN(8);
   else if (vec && nv <= 16) VTD_LN(16);
   else
-    hipLaunchKernelGGL((layernorm_generic_kernel<TI, TO>), grid, block, 0, st, x, rows, D, ldx,
-                       g, b, eps, yo, ldy);
+    hipLaunchKernelGGL((layernorm_generic_kernel<TI, TO, X3>), grid, block, 0, st, x, rows, D,
+                       ldx, g, b, eps, yo, ldy);
 #undef VTD_LN
   VTD_LAUNCH_CHECK("layernorm");
   return VTD_OK;
@@ -570,11 +600,13 @@ __global__ __launch_bounds__(256) void fold_ln_kernel(const float* __restrict__ 
 // tf.image.extract_patches(SAME, size = stride = p) + Reshape: output row m = b*N + t
 // (t = gy*gw + gx), column k = (kh*p + kw)*C + c; outside the image -> 0.
 // Each thread writes 8 consecutive output columns (one 16-B bf16 / 32-B f32 store).
-template <typename TO>
+// X3: TO = bf16_t, the split-bf16 operand (three ldo / 3 wide pieces)
+template <typename TO, bool X3 = false>
 __global__ __launch_bounds__(256) void patches_kernel(
     const float* __restrict__ img, int B, int H, int W, int C, int p, int gw, int N,
     int top, int left, int P, TO* __restrict__ out, int ldo) {
-  const int chunks = ldo / 8;
+  const int pw = X3 ? ldo / 3 : ldo;          // width of one piece
+  const int chunks = pw / 8;
   const int64_t total = (int64_t)B * N * chunks;
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
        g += (int64_t)gridDim.x * blockDim.x) {
@@ -597,7 +629,16 @@ __global__ __launch_bounds__(256) void patches_kernel(
       v[j] = val;
     }
     TO* o = out + m * ldo + k0;
-    if constexpr (sizeof(TO) == 2) {
+    if constexpr (X3) {
+      uint4 hi, lo;
+      hi.x = pack_bf16x2(v[0], v[1]); lo.x = pack_lo_bf16x2(v[0], v[1], hi.x);
+      hi.y = pack_bf16x2(v[2], v[3]); lo.y = pack_lo_bf16x2(v[2], v[3], hi.y);
+      hi.z = pack_bf16x2(v[4], v[5]); lo.z = pack_lo_bf16x2(v[4], v[5], hi.z);
+      hi.w = pack_bf16x2(v[6], v[7]); lo.w = pack_lo_bf16x2(v[6], v[7], hi.w);
+      *reinterpret_cast<uint4*>(o) = hi;
+      *reinterpret_cast<uint4*>(o + pw) = lo;
+      *reinterpret_cast<uint4*>(o + 2 * pw) = hi;
+    } else if constexpr (sizeof(TO) == 2) {
       bf16x8 w;
 #pragma unroll
       for (int j = 0; j < 8; ++j) w[j] = static_cast<short>(f32_to_bf16(v[j]));
@@ -631,6 +672,51 @@ __global__ __launch_bounds__(256) void patches_dense_kernel(
     const uint4 o = {pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3]),
                      pack_bf16x2(v1[0], v1[1]), pack_bf16x2(v1[2], v1[3])};
     *reinterpret_cast<uint4*>(out + m * (int64_t)(p * p * C) + kh * p * C + c8 * 8) = o;
+  }
+}
+
+// ------------------------------------------------------------------ split-bf16
+// f32 x [rows][ldx] (K columns) -> split-bf16 y [rows][ldy], three P = ldy / 3 wide pieces:
+// role 0 [hi | lo | hi] (A operand), role 1 [hi | hi | lo] (B operand); each thread 8 columns
+// of one row (16-B stores; columns [K, P) zero).  VEC: K % 8 == 0, ldx % 4 == 0, 16-B bases.
+template <bool VEC>
+__global__ __launch_bounds__(256) void split_bf16x3_kernel(const float* __restrict__ x,
+                                                           int64_t rows, int K, int ldx,
+                                                           bf16_t* __restrict__ y, int ldy,
+                                                           int role) {
+  const int P = ldy / 3, chunks = (P + 7) / 8;
+  const int64_t total = rows * chunks;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = g / chunks;
+    const int c0 = (int)(g - m * chunks) * 8;
+    const float* xr = x + m * ldx;
+    bf16_t* yr = y + m * ldy;
+    bf16_t* const pc1 = yr + P;                      // second piece
+    bf16_t* const pc2 = yr + 2 * P;                  // third piece
+    if (VEC && c0 + 8 <= P) {
+      f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = a;
+      if (c0 < K) {                                  // K % 8 == 0: all 8 or none
+        a = *reinterpret_cast<const f32x4*>(xr + c0);
+        b = *reinterpret_cast<const f32x4*>(xr + c0 + 4);
+      }
+      uint4 hi, lo;
+      hi.x = pack_bf16x2(a[0], a[1]); lo.x = pack_lo_bf16x2(a[0], a[1], hi.x);
+      hi.y = pack_bf16x2(a[2], a[3]); lo.y = pack_lo_bf16x2(a[2], a[3], hi.y);
+      hi.z = pack_bf16x2(b[0], b[1]); lo.z = pack_lo_bf16x2(b[0], b[1], hi.z);
+      hi.w = pack_bf16x2(b[2], b[3]); lo.w = pack_lo_bf16x2(b[2], b[3], hi.w);
+      *reinterpret_cast<uint4*>(yr + c0) = hi;
+      *reinterpret_cast<uint4*>(pc1 + c0) = role ? hi : lo;
+      *reinterpret_cast<uint4*>(pc2 + c0) = role ? lo : hi;
+    } else {
+      for (int c = c0; c < min(c0 + 8, P); ++c) {
+        const float v = c < K ? xr[c] : 0.f;
+        const bf16_t h = f32_to_bf16(v), l = lo_bf16(v, h);
+        yr[c] = h;
+        pc1[c] = role ? h : l;
+        pc2[c] = role ? l : h;
+      }
+    }
   }
 }
 
@@ -692,9 +778,16 @@ int layernorm_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx, c
                      hipStream_t st) {
   VTD_CHECK_ARG(x && g && b && y, "layernorm: null pointer");
   VTD_CHECK_ARG(rows > 0 && D > 0 && ldx >= D && ldy >= D, "layernorm: bad shape");
-  VTD_CHECK_ARG(dtype == VTD_F32 || dtype == VTD_BF16, "layernorm: bad dtype");
+  VTD_CHECK_ARG(dtype == VTD_F32 || dtype == VTD_BF16 || dtype == VTD_BF16X3,
+                "layernorm: bad dtype");
   VTD_CHECK_ARG(x_dtype == VTD_F32 || x_dtype == VTD_BF16, "layernorm: bad x dtype");
+  VTD_CHECK_ARG(dtype != VTD_BF16X3 || (ldy % 3 == 0 && ldy / 3 >= D),
+                "layernorm: a split-bf16 output needs ldy % 3 == 0 and ldy / 3 >= D");
   ProfScope ps(st, PROF_LN, 0.0);
+  if (dtype == VTD_BF16X3)
+    return x_dtype == VTD_BF16
+               ? ln_dispatch<bf16_t, bf16_t, true>(x, rows, D, ldx, g, b, eps, y, ldy, st)
+               : ln_dispatch<float, bf16_t, true>(x, rows, D, ldx, g, b, eps, y, ldy, st);
   if (x_dtype == VTD_BF16)
     return dtype == VTD_BF16 ? ln_dispatch<bf16_t, bf16_t>(x, rows, D, ldx, g, b, eps, y, ldy, st)
                              : ln_dispatch<bf16_t, float>(x, rows, D, ldx, g, b, eps, y, ldy, st);
@@ -828,11 +921,16 @@ int patches_launch(const float* img, int B, int H, int W, int C, int p, void* ou
   VTD_CHECK_ARG(B > 0 && H > 0 && W > 0 && C > 0 && p > 0, "extract_patches: bad shape");
   const int gh = (H + p - 1) / p, gw = (W + p - 1) / p;
   const int P = p * p * C;
-  VTD_CHECK_ARG(ldo >= P && ldo % 8 == 0, "extract_patches: ld_out must be >= P, % 8");
-  VTD_CHECK_ARG(dtype == VTD_F32 || dtype == VTD_BF16, "extract_patches: bad dtype");
+  VTD_CHECK_ARG(dtype == VTD_F32 || dtype == VTD_BF16 || dtype == VTD_BF16X3,
+                "extract_patches: bad dtype");
+  if (dtype == VTD_BF16X3)
+    VTD_CHECK_ARG(ldo % 24 == 0 && ldo / 3 >= P,
+                  "extract_patches: a split-bf16 output needs ld_out % 24 == 0, ld_out / 3 >= P");
+  else
+    VTD_CHECK_ARG(ldo >= P && ldo % 8 == 0, "extract_patches: ld_out must be >= P, % 8");
   const int pad_h = (gh - 1) * p + p - H, pad_w = (gw - 1) * p + p - W;
   const int N = gh * gw;
-  const int64_t total = (int64_t)B * N * (ldo / 8);
+  const int64_t total = (int64_t)B * N * ((dtype == VTD_BF16X3 ? ldo / 3 : ldo) / 8);
   const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
   ProfScope ps(st, PROF_PATCH, 0.0);
   if (dtype == VTD_BF16 && pad_h == 0 && pad_w == 0 && (p * C) % 8 == 0 && ldo == P &&
@@ -842,13 +940,37 @@ int patches_launch(const float* img, int B, int H, int W, int C, int p, void* ou
     const int gd = (int)std::min<int64_t>((tot + 255) / 256, 16384);
     hipLaunchKernelGGL(patches_dense_kernel, dim3(gd), dim3(256), 0, st, img, tot, H, W, C, p,
                        gw, N, static_cast<bf16_t*>(out));
-  } else if (dtype == VTD_BF16)
+  } else if (dtype == VTD_BF16X3)
+    hipLaunchKernelGGL((patches_kernel<bf16_t, true>), dim3(grid), dim3(256), 0, st, img, B, H,
+                       W, C, p, gw, N, pad_h / 2, pad_w / 2, P, static_cast<bf16_t*>(out), ldo);
+  else if (dtype == VTD_BF16)
     hipLaunchKernelGGL(patches_kernel<bf16_t>, dim3(grid), dim3(256), 0, st, img, B, H, W,
                        C, p, gw, N, pad_h / 2, pad_w / 2, P, static_cast<bf16_t*>(out), ldo);
   else
     hipLaunchKernelGGL(patches_kernel<float>, dim3(grid), dim3(256), 0, st, img, B, H, W,
                        C, p, gw, N, pad_h / 2, pad_w / 2, P, static_cast<float*>(out), ldo);
   VTD_LAUNCH_CHECK("extract_patches");
+  return VTD_OK;
+}
+
+int split_bf16x3_launch(const float* x, int64_t rows, int K, int ldx, void* y, int ldy, int role,
+                        hipStream_t st) {
+  VTD_CHECK_ARG(x && y && rows > 0 && K > 0 && ldx >= K, "split_bf16x3: bad arguments");
+  VTD_CHECK_ARG(ldy % 3 == 0 && ldy / 3 >= K && (role == 0 || role == 1),
+                "split_bf16x3: ldy % 3 == 0, ldy / 3 >= K, role 0 or 1");
+  ProfScope ps(st, PROF_OTHER, 0.0);
+  const int P = ldy / 3;
+  const int64_t total = rows * ((P + 7) / 8);
+  const int grid = (int)std::min<int64_t>((total + 255) / 256, 16384);
+  const bool vec = K % 8 == 0 && ldx % 4 == 0 && P % 8 == 0 &&
+                   reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(y) % 16 == 0;
+  if (vec)
+    hipLaunchKernelGGL(split_bf16x3_kernel<true>, dim3(grid), dim3(256), 0, st, x, rows, K, ldx,
+                       static_cast<bf16_t*>(y), ldy, role);
+  else
+    hipLaunchKernelGGL(split_bf16x3_kernel<false>, dim3(grid), dim3(256), 0, st, x, rows, K, ldx,
+                       static_cast<bf16_t*>(y), ldy, role);
+  VTD_LAUNCH_CHECK("split_bf16x3");
   return VTD_OK;
 }
 
@@ -905,6 +1027,12 @@ int vtd_extract_patches(const float* images_dev, int B, int H, int W, int C, int
                         void* out_dev, int ld_out, int dtype, void* stream) {
   return vtd::patches_launch(images_dev, B, H, W, C, p, out_dev, ld_out, dtype,
                              static_cast<hipStream_t>(stream));
+}
+
+int vtd_split_bf16x3(const float* x_dev, int64_t rows, int K, int ldx, void* y_dev, int ldy,
+                     int role, void* stream) {
+  return vtd::split_bf16x3_launch(x_dev, rows, K, ldx, y_dev, ldy, role,
+                                  static_cast<hipStream_t>(stream));
 }
 
 int vtd_decode(const float* logits_dev, int64_t n, float* dets_dev, void* stream) {

@@ -284,6 +284,18 @@ __device__ __forceinline__ void lds_read4_b64(const void* p, float2 (&o)[4]) {
       : "v"(a), "i"(O0), "i"(O1), "i"(O2), "i"(O3)
       : "memory");
 }
+// EPI_S3 (split-bf16 output): o = the hi words of v0, v1 already stored at idx; the lo
+// piece at idx + s3, hi again at idx + 2 s3 ([hi | lo | hi])
+__device__ __forceinline__ void store_s3(const EpiArgs& e, int64_t idx, const i32x4& o, f32x4 v0,
+                                         f32x4 v1) {
+  const i32x4 lo = {(int)pack_lo_bf16x2(v0[0], v0[1], (uint32_t)o[0]),
+                    (int)pack_lo_bf16x2(v0[2], v0[3], (uint32_t)o[1]),
+                    (int)pack_lo_bf16x2(v1[0], v1[1], (uint32_t)o[2]),
+                    (int)pack_lo_bf16x2(v1[2], v1[3], (uint32_t)o[3])};
+  bf16_t* p = static_cast<bf16_t*>(e.out) + idx;
+  store_out16(p + e.s3, lo);
+  store_out16(p + 2 * e.s3, o);
+}
 // TRL: the accumulators are in the transposed layout (lane (fr, fg): row 16 i + fr, columns
 // 32 jp + 8 fg .. + 7 in acc[i][2 jp], acc[i][2 jp + 1]): staged with ds_write_b128
 template <int EPI, int PR = 32, int DG = 0, typename PF = NoPF, bool TRL = false>
@@ -423,6 +435,7 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
                          (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
         if constexpr (DG & 4) asm volatile("" ::"v"(o));
         else store_out16(static_cast<bf16_t*>(e.out) + idx, o);
+        if constexpr ((EPI & EPI_S3) != 0) store_s3(e, idx, o, v0, v1);
         if constexpr (STAT) {      // the row's 64 columns live in 8 consecutive lanes
           // block mean, then the centred sum of squares (DPP sums, no LDS traffic)
           f32x2 pv[4];
@@ -832,6 +845,7 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
                            (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
           if constexpr (DG & 4) asm volatile("" ::"v"(o));
           else store_out16(static_cast<bf16_t*>(e.out) + idx, o);
+          if constexpr ((EPI & EPI_S3) != 0) store_s3(e, idx, o, v0, v1);
           if constexpr (STAT) {
             ob[jp] = o;
             tsum += bf16x8_sum(o);
@@ -1421,7 +1435,7 @@ int tile_group_width(int tiles_n) {
   X(0) X(1) X(2) X(4) X(5) X(6) X(8) X(9) X(10) X(12) X(13) X(14) X(EPI_PARTIAL)               \
   X(4 | EPI_LNF) X(5 | EPI_LNF) X(6 | EPI_LNF) X(4 | EPI_STAT) X(5 | EPI_STAT)                \
   X(6 | EPI_STAT) X(12 | EPI_STAT) X(13 | EPI_STAT) X(14 | EPI_STAT)                          \
-  X(4 | EPI_STAT | EPI_RA) X(4 | EPI_RA)
+  X(4 | EPI_STAT | EPI_RA) X(4 | EPI_RA) X(4 | EPI_S3) X(5 | EPI_S3) X(6 | EPI_S3)
 
 constexpr bool pp2_specialised(int code) {
 #define VTD_PP_IS(C) code == (C) ||
@@ -1433,6 +1447,7 @@ constexpr bool pp2_specialised(int code) {
 bool pp2_fast_epilogue(const vtd_epilogue* e) {
   auto al16 = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
   return e->bias && !e->detections && e->scatter_tokens <= 0 && e->ldo % 8 == 0 &&
+         (e->out_dtype != VTD_BF16X3 || (e->ldo / 3) % 8 == 0) &&
          (!e->resid || e->ldr % 8 == 0) && al16(e->out) && al16(e->bias) &&
          (!e->resid || al16(e->resid)) && (!e->out2 || (e->ldo2 % 8 == 0 && al16(e->out2)));
 }
@@ -1441,9 +1456,10 @@ bool pp2_fast_epilogue(const vtd_epilogue* e) {
 // EPI_GENERIC
 int pp2_code(const vtd_epilogue* e) {
   if (!pp2_fast_epilogue(e)) return EPI_GENERIC;
-  const int code = epi_code(e->act, e->out_dtype == VTD_BF16, e->resid != nullptr) |
+  const bool s3 = e->out_dtype == VTD_BF16X3;
+  const int code = epi_code(e->act, e->out_dtype == VTD_BF16 || s3, e->resid != nullptr) |
                    (e->lnstat ? EPI_LNF : 0) | (e->statout ? EPI_STAT : 0) |
-                   (e->rowadd ? EPI_RA : 0) | (e->out2 ? EPI_O2 : 0);
+                   (e->rowadd ? EPI_RA : 0) | (e->out2 ? EPI_O2 : 0) | (s3 ? EPI_S3 : 0);
   return pp2_specialised(code) ? code : EPI_GENERIC;
 }
 
@@ -1629,8 +1645,14 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
   VTD_CHECK_ARG(lda >= K && ldb >= K && lda % 8 == 0 && ldb % 8 == 0,
                 "gemm: lda/ldb must be >= K and multiples of 8");
   VTD_CHECK_ARG(dtype == VTD_F32 || dtype == VTD_BF16, "gemm: bad dtype");
-  VTD_CHECK_ARG(epi->out_dtype == VTD_F32 || epi->out_dtype == VTD_BF16,
-                "gemm: bad out dtype");
+  VTD_CHECK_ARG(epi->out_dtype == VTD_F32 || epi->out_dtype == VTD_BF16 ||
+                    (epi->out_dtype == VTD_BF16X3 && dtype == VTD_BF16),
+                "gemm: bad out dtype (VTD_BF16X3 output: bf16 operands only)");
+  VTD_CHECK_ARG(epi->out_dtype != VTD_BF16X3 ||
+                    (epi->ldo % 3 == 0 && epi->ldo / 3 >= N && !epi->out2 && !epi->detections &&
+                     !epi->resid && !epi->statout),
+                "gemm: a split-bf16 output needs ldo % 3 == 0, ldo / 3 >= N, no out2 / "
+                "detections / residual / statistics");
   VTD_CHECK_ARG(!epi->rowadd || epi->rowadd_period > 0, "gemm: rowadd_period");
   VTD_CHECK_ARG(epi->scatter_tokens <= 0 || N <= VTD_MAX_DETECT,
                 "gemm: scatter epilogue needs N <= 17");

@@ -82,6 +82,8 @@ struct EpiArgs {
   int tpw;
   // the tile order of ngw with precomputed divisors (set with ngw by the 256-tile launchers)
   TileOrder to;
+  // out_dtype VTD_BF16X3: width of one piece of the split-bf16 output row (ldo / 3)
+  int s3;
 };
 
 // bf16 output row vector store of the fast epilogues; build-time A/B knob VTD_OUT_NT: 1 =
@@ -235,8 +237,17 @@ __device__ __forceinline__ void epi_store(const EpiArgs& e, int M, int N, int m,
   } else {
     idx = (int64_t)m * e.ldo + n;
   }
-  if (e.out_dtype == VTD_F32) static_cast<float*>(e.out)[idx] = v;
-  else static_cast<bf16_t*>(e.out)[idx] = f32_to_bf16(v);
+  if (e.out_dtype == VTD_F32) {
+    static_cast<float*>(e.out)[idx] = v;
+  } else if (e.out_dtype == VTD_BF16X3) {         // [hi | lo | hi]
+    bf16_t* o = static_cast<bf16_t*>(e.out) + idx;
+    const bf16_t h = f32_to_bf16(v);
+    o[0] = h;
+    o[e.s3] = lo_bf16(v, h);
+    o[2 * e.s3] = h;
+  } else {
+    static_cast<bf16_t*>(e.out)[idx] = f32_to_bf16(v);
+  }
   if (e.out2) static_cast<bf16_t*>(e.out2)[(int64_t)m * e.ldo2 + n] = f32_to_bf16(v);
   if (e.dets) e.dets[(int64_t)m * 6 + n] = decode_transform(n, v);
 }
@@ -246,6 +257,7 @@ __device__ __forceinline__ void epi_store4(const EpiArgs& e, int M, int N, int m
                                            f32x4 v) {
   if (m >= M) return;
   const bool full = (n + 3 < N) && e.scatter_tokens <= 0 && !e.dets && (e.ldo & 3) == 0 &&
+                    (e.out_dtype != VTD_BF16X3 || (e.s3 & 3) == 0) &&
                     (!e.resid || (e.ldr & 3) == 0) && (!e.out2 || (e.ldo2 & 3) == 0);
   if (!full) {
 #pragma unroll
@@ -279,6 +291,13 @@ __device__ __forceinline__ void epi_store4(const EpiArgs& e, int M, int N, int m
   const int64_t idx = (int64_t)m * e.ldo + n;
   if (e.out_dtype == VTD_F32) {
     *reinterpret_cast<f32x4*>(static_cast<float*>(e.out) + idx) = v;
+  } else if (e.out_dtype == VTD_BF16X3) {
+    const uint32_t h0 = pack_bf16x2(v[0], v[1]), h1 = pack_bf16x2(v[2], v[3]);
+    bf16_t* o = static_cast<bf16_t*>(e.out) + idx;
+    *reinterpret_cast<uint2*>(o) = uint2{h0, h1};
+    *reinterpret_cast<uint2*>(o + e.s3) =
+        uint2{pack_lo_bf16x2(v[0], v[1], h0), pack_lo_bf16x2(v[2], v[3], h1)};
+    *reinterpret_cast<uint2*>(o + 2 * e.s3) = uint2{h0, h1};
   } else {
     bf16x4 o;
 #pragma unroll
@@ -304,6 +323,9 @@ constexpr int EPI_LNF = 32, EPI_STAT = 64, EPI_F8O = 128;
 // and the rare runtime modes: the position-embedding row add (patch embedding) and the bf16
 // copy of an f32 residual stream (out2)
 constexpr int EPI_RA = 256, EPI_O2 = 512;
+// the split-bf16 output (out_dtype VTD_BF16X3, with the bf16-output bit 4): [hi | lo | hi]
+// over three e.s3 wide pieces -- the next split-bf16 GEMM's A operand
+constexpr int EPI_S3 = 1024;
 __host__ __device__ constexpr int epi_code(int act, bool out_bf16, bool resid) {
   return act | (out_bf16 ? 4 : 0) | (resid ? 8 : 0);
 }
@@ -378,6 +400,7 @@ __host__ inline EpiArgs make_epi_args(const vtd_epilogue* epi) {
             epi->scatter_tokens, reinterpret_cast<const float2*>(epi->lnstat), epi->colsum,
             reinterpret_cast<float2*>(epi->statout), epi->stat_ld, epi->scale_out,
             epi->scale_rows, epi->detections};
+  e.s3 = epi->out_dtype == VTD_BF16X3 ? epi->ldo / 3 : 0;
   return e;
 }
 

@@ -41,6 +41,8 @@ int layernorm_mx8_launch(const void* x, int x_dtype, int64_t rows, int D, int ld
                          const float* g, const float* b, float eps, uint8_t* q, int ldq, int Kq,
                          uint8_t* s, int64_t s_rows, hipStream_t st);
 bool gemm_mx8_emits_fp8(int M, int N, const vtd_epilogue* e);
+int split_bf16x3_launch(const float* x, int64_t rows, int K, int ldx, void* y, int ldy, int role,
+                        hipStream_t st);
 int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_t* sA,
                     int64_t sa_rows, const uint8_t* Bt, int ldb, const uint8_t* sB,
                     int64_t sb_rows, const vtd_epilogue* epi, hipStream_t stream,
@@ -154,8 +156,9 @@ static int derive(const vtd_config* c, vtd_dims* d) {
   VTD_CHECK_ARG(c->head_last_units > 0 && c->head_layers > 0 && c->head_repeats > 0 &&
                     c->head_layers * c->head_repeats <= VTD_MAX_HEAD,
                 "bad mlp_head configuration");
-  VTD_CHECK_ARG(c->dtype == VTD_F32 || c->dtype == VTD_BF16 || c->dtype == VTD_FP8,
-                "dtype must be F32, BF16 or FP8");
+  VTD_CHECK_ARG(c->dtype == VTD_F32 || c->dtype == VTD_BF16 || c->dtype == VTD_FP8 ||
+                    c->dtype == VTD_BF16X3,
+                "dtype must be F32, BF16, FP8 or BF16X3");
   VTD_CHECK_ARG(c->key_dim <= 128, "encoder_key_dim > 128 not supported");
   const int p = c->patch_size;
   d->grid_h = (c->image_h + p - 1) / p;
@@ -199,14 +202,21 @@ static int derive(const vtd_config* c, vtd_dims* d) {
 
 namespace {
 struct Plan {
-  size_t patches, x, xb, h, stat, pstat, qkv, attn, mlp0, mlp1, u, head0, head1, q8, s8, q8b, s8b,
-      splitk, total;
+  size_t patches, x, xb, h, stat, pstat, qkv, attn, attn3, mlp0, mlp1, u, head0, head1, q8, s8, q8b,
+      s8b, splitk, total;
   int k8_max;                       // widest MX-fp8 GEMM K (VTD_FP8)
   int64_t s8_rows;                  // activation scale rows (rows rounded up to 4)
 };
-// activation / non-MX matrix dtype of a mode (VTD_FP8 keeps everything else in bf16)
-int act_dtype(int dtype) { return dtype == VTD_FP8 ? VTD_BF16 : dtype; }
+// activation / non-MX matrix dtype of a mode (VTD_FP8 keeps everything else in bf16; the
+// split-bf16 mode VTD_BF16X3 keeps its activations -- query/key/value, attention -- in f32)
+int act_dtype(int dtype) {
+  return dtype == VTD_FP8 ? VTD_BF16 : dtype == VTD_BF16X3 ? VTD_F32 : dtype;
+}
 size_t es_of(int dtype) { return act_dtype(dtype) == VTD_BF16 ? 2 : 4; }
+// GEMM A operands (patches, LayerNorm out, MLP / head activations): bytes per logical element
+// (VTD_BF16X3: three bf16 pieces) and the operand width of a K-wide logical row
+size_t eop_of(int dtype) { return dtype == VTD_BF16X3 ? 6 : es_of(dtype); }
+int opk(int dtype, int k) { return dtype == VTD_BF16X3 ? 3 * k : k; }
 // dtype of the residual stream x: bf16 in the bf16 / fp8 modes (the stream the GEMM
 // epilogues add into and the LayerNorms read), f32 in the f32 mode.  VTD_RESID_F32=1
 // keeps an f32 stream in the bf16 modes (A/B diagnostic; costs ~7 % at C2).
@@ -226,28 +236,31 @@ Plan make_plan(const vtd_config* c, const vtd_dims& d) {
     off += (bytes + 255) / 256 * 256;
     return o;
   };
-  const size_t es = es_of(c->dtype);
+  const size_t es = es_of(c->dtype), eop = eop_of(c->dtype);
   const size_t R = (size_t)d.rows, HR = (size_t)d.head_rows;
   int mlp_max = 0, head_max = 0;
   for (int j = 0; j < c->mlp_quantities; ++j) mlp_max = std::max(mlp_max, d.mlp_units_p[j]);
   for (int j = 0; j < d.n_head; ++j) head_max = std::max(head_max, d.head_units_p[j]);
-  p.patches = take(R * d.patch_dim_p * es);
+  p.patches = take(R * d.patch_dim_p * eop);
   p.x = take(R * d.d_p * 4);
   p.xb = take(act_dtype(c->dtype) == VTD_BF16 ? R * d.d_p * 2 : 0);
-  p.h = take(R * d.d_p * es);
+  p.h = take(R * d.d_p * eop);
   p.stat = take(R * 8);                 // LayerNorm (mean, rstd) per row, fold path
   p.pstat = take(R * (d.d_p / 64) * 8);  // producer partial (sum, sumsq) per 64 columns
   p.qkv = take(R * d.qkv_p * es);
   p.attn = take(R * d.inner_p * es);
-  p.mlp0 = take(R * mlp_max * es);
-  p.mlp1 = take(R * mlp_max * es);
-  p.u = take(HR * d.tokens_p * es);
-  p.head0 = take(HR * head_max * es);
-  p.head1 = take(HR * head_max * es);
+  // VTD_BF16X3: the attention output as the split-bf16 operand of attention_output
+  p.attn3 = take(c->dtype == VTD_BF16X3 ? R * d.inner_p * eop : 0);
+  p.mlp0 = take(R * mlp_max * eop);
+  p.mlp1 = take(R * mlp_max * eop);
+  p.u = take(HR * d.tokens_p * eop);
+  p.head0 = take(HR * head_max * eop);
+  p.head1 = take(HR * head_max * eop);
   // fp32 split-K partials of the head's few-tile, long-K Dense layers (gemm_splitk_choice)
   size_t sk = 0;
   for (int j = 0, k = d.tokens_p; j < d.n_head; k = d.head_units_p[j], ++j) {
-    const int s = gemm_splitk_choice((int)HR, d.head_units_p[j], k, act_dtype(c->dtype));
+    const int s = gemm_splitk_choice((int)HR, d.head_units_p[j], opk(c->dtype, k),
+                                     c->dtype == VTD_BF16X3 ? VTD_BF16 : act_dtype(c->dtype));
     if (s > 1) sk = std::max(sk, (size_t)s * HR * d.head_units_p[j] * 4);
   }
   p.splitk = take(sk);
@@ -487,6 +500,11 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   const Plan P = make_plan(cfg, d);
   const bool fp8 = cfg->dtype == VTD_FP8;
   const int dt = act_dtype(cfg->dtype);
+  // VTD_BF16X3: every GEMM runs on split-bf16 operands (bf16 kernels over K' = 3 K_p), whose
+  // A operands the producers write directly (odt); qkv / attention / x stay f32
+  const bool x3 = cfg->dtype == VTD_BF16X3;
+  const int gdt = x3 ? VTD_BF16 : dt, odt = x3 ? VTD_BF16X3 : dt;
+  auto kk = [&](int k) { return opk(cfg->dtype, k); };
   const int B = cfg->batch, N = d.tokens, D = d.d, Dp = d.d_p;
   const int64_t R = d.rows;
   VTD_CHECK_ARG(R < (int64_t)1 << 31, "forward: batch*tokens too large");
@@ -543,7 +561,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   // against the MX-fp8 weights (W [Np][K8], S [K8/128][Np][4])
   auto enc_gemm = [&](int Np, int K, const void* a, const void* W, const uint8_t* S,
                       const vtd_epilogue* e, double flops) -> int {
-    if (!fp8) return gemm_launch(M, Np, K, a, K, W, K, dt, e, st, flops);
+    if (!fp8) return gemm_launch(M, Np, kk(K), a, kk(K), W, kk(K), gdt, e, st, flops);
     const int K8 = k8_of(K);
     int r = quantize_mx8_launch(a, VTD_BF16, R, K, K, K8, q8, K8, s8, P.s8_rows, st);
     if (r) return r;
@@ -569,7 +587,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   if (s_lo <= 0 && 0 < s_hi) {
   // ---- ExtractImagePatches + flatten (vtd.py:271-280)
   rc = patches_launch(images, B, cfg->image_h, cfg->image_w, cfg->channels,
-                      cfg->patch_size, patches, d.patch_dim_p, dt, st);
+                      cfg->patch_size, patches, kk(d.patch_dim_p), odt, st);
   if (rc) return rc;
   // ---- linear_projection + position embedding add (vtd.py:291-307)
   {
@@ -579,8 +597,8 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     e.act = VTD_ACT_NONE;
     e.out = x; e.ldo = Dp; e.out_dtype = rdt;
     emit_stats(e, cfg->repeat_times > 0 && w->layers[0].ln1_colsum);
-    rc = gemm_launch(M, Dp, d.patch_dim_p, patches, d.patch_dim_p, w->w_patch,
-                     d.patch_dim_p, dt, &e, st, 2.0 * fR * D * d.patch_dim);
+    rc = gemm_launch(M, Dp, kk(d.patch_dim_p), patches, kk(d.patch_dim_p), w->w_patch,
+                     kk(d.patch_dim_p), gdt, &e, st, 2.0 * fR * D * d.patch_dim);
     if (rc) return rc;
   }
   }
@@ -603,7 +621,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     } else if (fp8) {
       rc = ln_mx8(L.ln1_gamma, L.ln1_beta);       // LayerNorm + MX quantization, one pass
     } else {
-      rc = layernorm_launch(x, rdt, R, D, Dp, L.ln1_gamma, L.ln1_beta, 1e-3f, h, Dp, dt, st);
+      rc = layernorm_launch(x, rdt, R, D, Dp, L.ln1_gamma, L.ln1_beta, 1e-3f, h, kk(Dp), odt, st);
     }
     if (rc) return rc;
     {
@@ -625,6 +643,14 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
                   : attention_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale,
                                      attn, d.inner_p, dt, st, attn_flops);
     if (rc) return rc;
+    // VTD_BF16X3: the f32 attention output split into the attention_output GEMM's operand
+    const void* attn_op = attn;
+    if (x3) {
+      rc = split_bf16x3_launch(static_cast<const float*>(attn), R, d.inner_p, d.inner_p,
+                               ws + P.attn3, kk(d.inner_p), 0, st);
+      if (rc) return rc;
+      attn_op = ws + P.attn3;
+    }
     {
       vtd_epilogue e{};
       e.bias = L.b_out; e.act = VTD_ACT_NONE;
@@ -633,7 +659,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
       emit_stats(e, L.ln2_colsum != nullptr);
       const double fl = 2.0 * fR * cfg->num_heads * cfg->key_dim * D;
       rc = attn_mx8 ? mx_gemm(Dp, d.inner_p, q8, s8, L.w_out, L.s_out, &e, fl)
-                    : enc_gemm(Dp, d.inner_p, attn, L.w_out, L.s_out, &e, fl);
+                    : enc_gemm(Dp, d.inner_p, attn_op, L.w_out, L.s_out, &e, fl);
       if (rc) return rc;
     }
     const void* a = h;
@@ -647,7 +673,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
       rc = ln_mx8(L.ln2_gamma, L.ln2_beta);
       aq = q8; as = s8;
     } else {
-      rc = layernorm_launch(x, rdt, R, D, Dp, L.ln2_gamma, L.ln2_beta, 1e-3f, h, Dp, dt, st);
+      rc = layernorm_launch(x, rdt, R, D, Dp, L.ln2_gamma, L.ln2_beta, 1e-3f, h, kk(Dp), odt, st);
     }
     if (rc) return rc;
     int k = Dp, kv = D;
@@ -664,7 +690,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
         }
         emit_stats(e, i + 1 < cfg->repeat_times && w->layers[i + 1].ln1_colsum);
       } else {
-        e.out = mlp[j & 1]; e.ldo = d.mlp_units_p[j]; e.out_dtype = dt;
+        e.out = mlp[j & 1]; e.ldo = kk(d.mlp_units_p[j]); e.out_dtype = odt;
       }
       // VTD_FP8: an inner MLP layer writes the next layer's MX-fp8 operand itself (into the
       // operand buffer it is not reading) when every tile takes the fast epilogue
@@ -695,14 +721,18 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   if (diag_nohead) return VTD_OK;
   // ---- mlp_head: Dense(17) + Reshape((17, -1)) as a scatter epilogue (vtd.py:454-463)
   {
-    const size_t es = es_of(dt);
-    VTD_HIP(hipMemsetAsync(u, 0, (size_t)d.head_rows * d.tokens_p * es, st));
+    VTD_HIP(hipMemsetAsync(u, 0, (size_t)d.head_rows * d.tokens_p * eop_of(cfg->dtype), st));
     vtd_epilogue e{};
     e.bias = w->b_det; e.act = VTD_ACT_NONE;
-    e.out = u; e.ldo = d.tokens_p; e.out_dtype = dt;
+    e.out = u; e.ldo = kk(d.tokens_p); e.out_dtype = odt;
     e.scatter_tokens = N;
     const void* a = dt == rdt ? x : xb;
-    rc = gemm_launch(M, VTD_MAX_DETECT, Dp, a, Dp, w->w_det, Dp, dt, &e, st,
+    if (x3) {                        // the f32 stream x as the split-bf16 operand (h is free)
+      rc = split_bf16x3_launch(static_cast<const float*>(x), R, Dp, Dp, h, kk(Dp), 0, st);
+      if (rc) return rc;
+      a = h;
+    }
+    rc = gemm_launch(M, VTD_MAX_DETECT, kk(Dp), a, kk(Dp), w->w_det, kk(Dp), gdt, &e, st,
                      2.0 * fR * D * VTD_MAX_DETECT);
     if (rc) return rc;
   }
@@ -712,12 +742,13 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   for (int j = 0; j < d.n_head; ++j) {                // vtd.py:468-486
     vtd_epilogue e{};
     e.bias = w->b_head[j]; e.act = act;
-    e.out = head[j & 1]; e.ldo = d.head_units_p[j]; e.out_dtype = dt;
+    e.out = head[j & 1]; e.ldo = kk(d.head_units_p[j]); e.out_dtype = odt;
     const double fl = 2.0 * HR * (double)kv * d.head_units[j];
-    const int ks = gemm_splitk_choice(HR, d.head_units_p[j], k, dt);
-    rc = ks > 1 ? gemm_splitk_launch(HR, d.head_units_p[j], k, a, k, w->w_head[j], k, &e,
-                                     reinterpret_cast<float*>(ws + P.splitk), ks, st, fl)
-                : gemm_launch(HR, d.head_units_p[j], k, a, k, w->w_head[j], k, dt, &e, st, fl);
+    const int ks = gemm_splitk_choice(HR, d.head_units_p[j], kk(k), gdt);
+    rc = ks > 1 ? gemm_splitk_launch(HR, d.head_units_p[j], kk(k), a, kk(k), w->w_head[j], kk(k),
+                                     &e, reinterpret_cast<float*>(ws + P.splitk), ks, st, fl)
+                : gemm_launch(HR, d.head_units_p[j], kk(k), a, kk(k), w->w_head[j], kk(k), gdt,
+                              &e, st, fl);
     if (rc) return rc;
     a = head[j & 1];
     k = d.head_units_p[j];
@@ -728,7 +759,8 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     e.bias = w->b_final; e.act = VTD_ACT_NONE;
     e.out = logits; e.ldo = 6; e.out_dtype = VTD_F32;
     e.detections = dets;                              // transform_predictions, fused
-    rc = gemm_launch(HR, 6, k, a, k, w->w_final, k, dt, &e, st, 2.0 * HR * (double)kv * 6);
+    rc = gemm_launch(HR, 6, kk(k), a, kk(k), w->w_final, kk(k), gdt, &e, st,
+                     2.0 * HR * (double)kv * 6);
     if (rc) return rc;
   }
   return VTD_OK;

@@ -38,9 +38,12 @@ class Constants(Enum):                                   # vtd.py:19-43
 
 
 _DTYPES = {"float32": L.F32, "fp32": L.F32, "f32": L.F32, "bfloat16": L.BF16,
-           "bf16": L.BF16, "float8": L.FP8, "fp8": L.FP8, "mxfp8": L.FP8}
-# storage dtype of the activations and of the matrices outside the MX-fp8 layers
-_TORCH_DTYPE = {L.F32: torch.float32, L.BF16: torch.bfloat16, L.FP8: torch.bfloat16}
+           "bf16": L.BF16, "float8": L.FP8, "fp8": L.FP8, "mxfp8": L.FP8,
+           "bfloat16x3": L.BF16X3, "bf16x3": L.BF16X3, "split_bf16": L.BF16X3}
+# storage dtype of the activations and of the matrices outside the MX-fp8 layers (the
+# split-bf16 mode stores its matrices as bf16 rows of three pieces, include/vtd.h)
+_TORCH_DTYPE = {L.F32: torch.float32, L.BF16: torch.bfloat16, L.FP8: torch.bfloat16,
+                L.BF16X3: torch.bfloat16}
 
 
 def _resolve_dtype(dtype) -> int:
@@ -49,8 +52,9 @@ def _resolve_dtype(dtype) -> int:
     try:
         return _DTYPES[str(dtype).lower()]
     except KeyError:
-        raise ValueError(f"unsupported dtype {dtype!r}: use 'float32' (parity), 'bfloat16' "
-                         "or 'float8' (MX-fp8 encoder Dense layers)")
+        raise ValueError(f"unsupported dtype {dtype!r}: use 'float32' (parity), 'bf16x3' "
+                         "(split-bf16 parity mode), 'bfloat16' or 'float8' (MX-fp8 encoder "
+                         "Dense layers)")
 
 
 # ------------------------------------------------------------------------- names
@@ -235,6 +239,7 @@ class Model:
     def _pack(self):
         dims = self.dims
         fp8 = self.dtype == L.FP8
+        x3 = self.dtype == L.BF16X3             # split-bf16: packed in f32, then split
         dt = L.BF16 if fp8 else self.dtype      # dtype of the non-MX matrices
         tdt = _TORCH_DTYPE[dt]
         dev = self.device
@@ -251,8 +256,19 @@ class Model:
             staging.append(t)
             return t
 
+        def split3(w32):
+            """split-bf16 B operand [hi | hi | lo] of a packed fp32 matrix [rows_p][k_p]."""
+            rows_p, k_p = w32.shape
+            out = zeros(rows_p, 3 * k_p, dtype=torch.bfloat16)
+            L.check(L.lib.vtd_split_bf16x3(w32.data_ptr(), rows_p, k_p, k_p, out.data_ptr(),
+                                           3 * k_p, 1, stream), "split_bf16x3")
+            return out
+
         def dense(name, rows_p, k_p, kg=None, kgp=None, ng=None, ngp=None, dst=None, off=0,
                   pdt=None):
+            if x3 and dst is None and pdt is None:
+                return split3(dense(name, rows_p, k_p, kg, kgp, ng, ngp,
+                                    dst=f32_staging(rows_p, k_p), off=off, pdt=L.F32))
             w = src(name + "/kernel")
             w2 = w.reshape(-1, w.shape[-1]) if w.dim() == 3 and kg is not None else w.reshape(w.shape[0], -1)
             K, N = w2.shape
@@ -337,16 +353,18 @@ class Model:
             g2, b2 = vector(f"{ln2}/gamma", dims.d_p), vector(f"{ln2}/beta", dims.d_p)
             Ly.ln1_gamma, Ly.ln1_beta = g1.data_ptr(), b1.data_ptr()
             Ly.ln2_gamma, Ly.ln2_beta = g2.data_ptr(), b2.data_ptr()
-            wqkv = (f32_staging(dims.qkv_p, dims.d_p) if fp8 or fold
+            wqkv = (f32_staging(dims.qkv_p, dims.d_p) if fp8 or fold or x3
                     else zeros(dims.qkv_p, dims.d_p))
             bqkv = zeros(dims.qkv_p, dtype=torch.float32)
             for part_i, part in enumerate(("query", "key", "value")):
                 off = part_i * dims.inner_p
                 # EinsumDense kernel (D, H, dk) -> (D, H*dk); columns padded per head
                 dense(f"{mha}/{part}", None, dims.d_p, ng=dk, ngp=dkp, dst=wqkv, off=off,
-                      pdt=L.F32 if fp8 or fold else None)
+                      pdt=L.F32 if fp8 or fold or x3 else None)
                 vector(f"{mha}/{part}/bias", None, ng=dk, ngp=dkp, dst=bqkv, off=off)
-            Ly.w_qkv, Ly.s_qkv = mx8(wqkv, f"{mha}/qkv") if fp8 else (wqkv.data_ptr(), None)
+            Ly.w_qkv, Ly.s_qkv = (mx8(wqkv, f"{mha}/qkv") if fp8 else
+                                  (split3(wqkv).data_ptr(), None) if x3 else
+                                  (wqkv.data_ptr(), None))
             Ly.b_qkv = bqkv.data_ptr()
             if fold:
                 Ly.w_qkv, Ly.b_qkv, Ly.ln1_colsum = fold_ln(wqkv, bqkv, g1, b1)
