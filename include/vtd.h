@@ -202,9 +202,9 @@ typedef struct vtd_epilogue {
    * (acc - mean * colsum[n]) * rstd before bias / act.  Both NULL: no fold. */
   const float* lnstat; const float* colsum;
   /* Partial LayerNorm statistics of the output (the fold path's producer side): for row m
-   * and 64-column block b, statout[2 (m stat_ld + b)] = mean and [.. + 1] = sum of squared
+   * and 64-column block b, statout[2 (b stat_ld + m)] = mean and [.. + 1] = sum of squared
    * deviations from that mean, of the block's 64 stored bf16 values (centred partials:
-   * exact whatever |mean| / std).  Only on full 256 x 256 tiles of the bf16 fast epilogues
+   * exact whatever |mean| / std).  Slot-major: one plane of stat_ld >= M rows per block.  Only on full 256 x 256 tiles of the bf16 fast epilogues
    * (else vtd_gemm returns VTD_ERR_UNSUPPORTED); NULL: none. */
   float* statout; int stat_ld;
   /* out_dtype VTD_FP8 (vtd_gemm_mx8 only, every tile full: M % 256 == N % 256 == 0): the
@@ -267,8 +267,9 @@ int vtd_layernorm_stats(const void* x_dev, int x_dtype, int64_t rows, int D, int
                         float eps, float* stat_dev, void* stream);
 
 /* (mean, rstd) per row from the centred partials a producer GEMM wrote
- * (vtd_epilogue.statout, `slots` 64-column blocks per row, D == 64 * slots): Chan's merge
- * of the block (mean, M2) pairs in fp32, no one-pass sum(x^2) - mean^2 cancellation. */
+ * (vtd_epilogue.statout with stat_ld == rows: `slots` planes of `rows` (mean, M2) pairs,
+ * D == 64 * slots): Chan's merge of the block (mean, M2) pairs in fp32, no one-pass
+ * sum(x^2) - mean^2 cancellation. */
 int vtd_layernorm_stats_finalize(const float* partial_dev, int64_t rows, int slots, int D,
                                  float eps, float* stat_dev, void* stream);
 

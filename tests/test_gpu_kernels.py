@@ -478,9 +478,10 @@ def test_gemm_accumulator_layouts(L, cuda, act, resid, fold, stat, tr):
         keep += [lnstat, colsum]
         e.lnstat, e.colsum = lnstat.data_ptr(), colsum.data_ptr()
     if stat:
-        st = torch.full((M, N // 64, 2), float("nan"), device=cuda)
-        keep.append(st)
-        e.statout, e.stat_ld = st.data_ptr(), N // 64
+        st_planes = torch.full((N // 64, M, 2), float("nan"), device=cuda)   # slot-major statout
+        st = st_planes.permute(1, 0, 2)
+        keep.append(st_planes)
+        e.statout, e.stat_ld = st_planes.data_ptr(), M
     with L.knob(L.KNOB_GEMM_TR, tr):
         L.check(L.lib.vtd_gemm(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, L.BF16,
                                ctypes.byref(e), L.stream_ptr()), "vtd_gemm")
@@ -515,10 +516,11 @@ def test_gemm_statout_variants(L, cuda, monkeypatch, variant):
     Bt = (torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
     bias = torch.randn(N, generator=g, device=cuda)
     out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
-    stat = torch.full((M, N // 64, 2), float("nan"), device=cuda)
+    stat_planes = torch.full((N // 64, M, 2), float("nan"), device=cuda)   # slot-major statout
+    stat = stat_planes.permute(1, 0, 2)
     e = L.VtdEpilogue()
     e.bias, e.out, e.ldo, e.out_dtype = bias.data_ptr(), out.data_ptr(), N, 1
-    e.statout, e.stat_ld = stat.data_ptr(), N // 64
+    e.statout, e.stat_ld = stat_planes.data_ptr(), M
     L.check(L.lib.vtd_gemm(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, L.BF16,
                            ctypes.byref(e), L.stream_ptr()), "vtd_gemm")
     torch.cuda.synchronize()
@@ -711,21 +713,22 @@ def test_gemm_statout_and_finalize(L, cuda, N, K, act, resid, offset):
         bias += offset if act == 0 else 0.0
     x = (offset + 2 * torch.randn(M, N, generator=g, device=cuda)).to(torch.bfloat16)
     slots = N // 64
-    part = torch.full((M, slots, 2), float("nan"), device=cuda)
+    part_planes = torch.full((slots, M, 2), float("nan"), device=cuda)   # slot-major statout
+    part = part_planes.permute(1, 0, 2)
     e = L.VtdEpilogue()
     e.bias, e.act, e.out, e.ldo, e.out_dtype = bias.data_ptr(), act, x.data_ptr(), N, 1
     if resid:
         e.resid, e.ldr = x.data_ptr(), N
-    e.statout, e.stat_ld = part.data_ptr(), slots
+    e.statout, e.stat_ld = part_planes.data_ptr(), M
     L.check(L.lib.vtd_gemm(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, L.BF16, ctypes.byref(e),
                            L.stream_ptr()), "gemm")
     st = torch.zeros(M, 2, device=cuda)
-    L.check(L.lib.vtd_layernorm_stats_finalize(part.data_ptr(), M, slots, N, 1e-3, st.data_ptr(),
+    L.check(L.lib.vtd_layernorm_stats_finalize(part_planes.data_ptr(), M, slots, N, 1e-3, st.data_ptr(),
                                                L.stream_ptr()), "finalize")
     # the grid-stride form (knob VTD_KNOB_FIN_WGS, few 1024-thread workgroups): same bits
     st2 = torch.full((M, 2), float("nan"), device=cuda)
     with L.knob(L.KNOB_FIN_WGS, 3):
-        L.check(L.lib.vtd_layernorm_stats_finalize(part.data_ptr(), M, slots, N, 1e-3,
+        L.check(L.lib.vtd_layernorm_stats_finalize(part_planes.data_ptr(), M, slots, N, 1e-3,
                                                    st2.data_ptr(), L.stream_ptr()), "finalize")
     torch.cuda.synchronize()
     assert torch.equal(st, st2)
@@ -761,10 +764,10 @@ def test_gemm_statout_unsupported_shape(L, cuda):
     Bt = torch.zeros(N, K, device=cuda, dtype=torch.bfloat16)
     out = torch.zeros(M, N, device=cuda, dtype=torch.bfloat16)
     bias = torch.zeros(N, device=cuda)
-    part = torch.zeros(M, N // 64, 2, device=cuda)
+    part_planes = torch.zeros(N // 64, M, 2, device=cuda)     # slot-major statout
     e = L.VtdEpilogue()
     e.bias, e.out, e.ldo, e.out_dtype = bias.data_ptr(), out.data_ptr(), N, 1
-    e.statout, e.stat_ld = part.data_ptr(), N // 64
+    e.statout, e.stat_ld = part_planes.data_ptr(), M
     with pytest.raises(L.VtdError):
         L.check(L.lib.vtd_gemm(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, L.BF16, ctypes.byref(e),
                                L.stream_ptr()), "gemm")
@@ -836,12 +839,13 @@ def test_gemm_statout_needs_a_specialised_epilogue(L, cuda):
     colsum = Bt.float().sum(1).contiguous()
     lnstat = torch.stack([A.float().mean(1), torch.ones(M, device=cuda)], 1).contiguous()
     x = torch.randn(M, N, generator=g, device=cuda).to(torch.bfloat16)
-    stat = torch.full((M, N // 64, 2), float("nan"), device=cuda)
+    stat_planes = torch.full((N // 64, M, 2), float("nan"), device=cuda)   # slot-major statout
+    stat = stat_planes.permute(1, 0, 2)
     e = L.VtdEpilogue()
     e.bias, e.act, e.out, e.ldo, e.out_dtype = bias.data_ptr(), L.ACT_GELU_TANH, x.data_ptr(), N, 1
     e.resid, e.ldr = x.data_ptr(), N
     e.lnstat, e.colsum = lnstat.data_ptr(), colsum.data_ptr()
-    e.statout, e.stat_ld = stat.data_ptr(), N // 64
+    e.statout, e.stat_ld = stat_planes.data_ptr(), M
     rc = L.lib.vtd_gemm(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, L.BF16, ctypes.byref(e),
                         L.stream_ptr())
     assert rc == -2, (rc, L.lib.vtd_last_error())
@@ -888,8 +892,9 @@ def test_gemm_tiles_per_workgroup(L, cuda, M, N, K, act, mode, tpw):
         if mode in ("f32resid", "stat"):
             e.resid, e.ldr = x.data_ptr(), N
         if mode == "stat":
-            st = torch.full((M, N // 64, 2), float("nan"), device=cuda)
-            e.statout, e.stat_ld = st.data_ptr(), N // 64
+            st_planes = torch.full((N // 64, M, 2), float("nan"), device=cuda)   # slot-major statout
+            st = st_planes.permute(1, 0, 2)
+            e.statout, e.stat_ld = st_planes.data_ptr(), M
         if mode == "fold":
             gg = torch.Generator(device=cuda).manual_seed(3)
             lnstat = torch.stack([torch.randn(M, generator=gg, device=cuda) * 0.1,

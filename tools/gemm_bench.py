@@ -100,9 +100,12 @@ def run(name, spec, reps, dev):
         e.resid, e.ldr = out.data_ptr(), N
     keep = []
     if name in STATOUT:
+        # slot-major planes (stat_ld = M, round 5); VTD_STAT_ROWMAJOR=1 for a library built
+        # before (stat_ld = N / 64): the same buffer size either way
         stat = torch.empty(M, N // 64, 2, device=dev)
         keep.append(stat)
-        e.statout, e.stat_ld = stat.data_ptr(), N // 64
+        e.statout = stat.data_ptr()
+        e.stat_ld = N // 64 if os.environ.get("VTD_STAT_ROWMAJOR") == "1" else M
     if name in LNFOLD:
         lnstat = torch.stack([torch.zeros(M, device=dev), torch.ones(M, device=dev)], 1).contiguous()
         colsum = Bt.float().sum(1).contiguous()

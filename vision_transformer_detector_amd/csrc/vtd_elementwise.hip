@@ -523,18 +523,18 @@ __global__ __launch_bounds__(256) void ln_stats_finalize_kernel(const float2* __
                                                                 float2* __restrict__ stat) {
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (r >= rows) return;
-  const float2* pr = part + r * slots;
+  const float2* pr = part + r;                    // slot b at pr[b * rows]
   const float m0 = pr[0].x;
   float ds = 0.f, q = 0.f;
   for (int b = 0; b < slots; ++b) {
-    const float2 t = pr[b];
+    const float2 t = pr[b * rows];
     ds += t.x - m0;
     q += t.y;
   }
   const float dmean = ds / slots;
   float between = 0.f;
   for (int b = 0; b < slots; ++b) {
-    const float dv = (pr[b].x - m0) - dmean;
+    const float dv = (pr[b * rows].x - m0) - dmean;
     between += dv * dv;
   }
   const float var = (q + 64.f * between) / D;
@@ -548,16 +548,18 @@ __global__ __launch_bounds__(256) void ln_stats_finalize_kernel(const float2* __
 // workgroups in the two-stream forward, where every workgroup waits for a CU the other
 // stream's GEMM tile vacates (knob VTD_KNOB_FIN_WGS).
 template <int S>
-__global__ __launch_bounds__(1024) void ln_stats_finalize_s_kernel(const float4* __restrict__ part,
+__global__ __launch_bounds__(1024) void ln_stats_finalize_s_kernel(const float2* __restrict__ part,
                                                                    int64_t rows, int D, float eps,
                                                                    float2* __restrict__ stat) {
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows;
        r += (int64_t)gridDim.x * blockDim.x) {
+    // slot-major planes: slot b of row r at part[b * rows + r] (a wave's loads are 512
+    // contiguous bytes per slot)
     f32x4 v[S / 2];
 #pragma unroll
     for (int b = 0; b < S / 2; ++b) {
-      const float4 w = part[r * (S / 2) + b];
-      v[b] = f32x4{w.x, w.y, w.z, w.w};
+      const float2 w0 = part[(2 * b) * rows + r], w1 = part[(2 * b + 1) * rows + r];
+      v[b] = f32x4{w0.x, w0.y, w1.x, w1.y};
     }
     stat[r] = ln_merge_partials<S>(v, D, eps);
   }
@@ -872,20 +874,20 @@ int ln_stats_finalize_launch(const float* part, int64_t rows, int slots, int D, 
   VTD_CHECK_ARG(reinterpret_cast<uintptr_t>(part) % 8 == 0 && reinterpret_cast<uintptr_t>(stat) % 8 == 0,
                 "layernorm_stats_finalize: alignment");
   ProfScope ps(st, PROF_LN, 0.0);
-  // the common widths: every partial loaded at once (16-B loads), one memory round trip
+  // the common widths: every partial loaded at once, one memory round trip
   if (slots == 12 || slots == 16) {
-    if (reinterpret_cast<uintptr_t>(part) % 16 == 0) {
+    {
       auto k = slots == 12 ? ln_stats_finalize_s_kernel<12> : ln_stats_finalize_s_kernel<16>;
       // knob VTD_KNOB_FIN_WGS = n > 0: n workgroups of 1024 threads (grid-stride)
       const int fw = knob(VTD_KNOB_FIN_WGS);
       const int64_t need = (rows + 1023) / 1024;
       if (fw > 0)
         hipLaunchKernelGGL(k, dim3((unsigned)std::min<int64_t>(fw, need)), dim3(1024), 0, st,
-                           reinterpret_cast<const float4*>(part), rows, D, eps,
+                           reinterpret_cast<const float2*>(part), rows, D, eps,
                            reinterpret_cast<float2*>(stat));
       else
         hipLaunchKernelGGL(k, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st,
-                           reinterpret_cast<const float4*>(part), rows, D, eps,
+                           reinterpret_cast<const float2*>(part), rows, D, eps,
                            reinterpret_cast<float2*>(stat));
       VTD_LAUNCH_CHECK("layernorm_stats_finalize");
       return VTD_OK;

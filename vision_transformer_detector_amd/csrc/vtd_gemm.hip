@@ -376,6 +376,10 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
       else lds_read4_b64<768, 832, 896, 960>(lst + rsub, stv);
     }
     f32x4 rv[NIT][2];
+    // STAT: lanes with (lane & 7) == it keep row it * 8 + rsub's (mean, M2): after the pass,
+    // lanes (lane & 7) < NIT hold 32 distinct rows, stored by ONE instruction (the slot-major
+    // statout plane makes them 256 contiguous bytes)
+    [[maybe_unused]] float2 stkeep = float2{0.f, 0.f};
     if constexpr (RESID && !RPRE) {
 #pragma unroll
       for (int it = 0; it < NIT; ++it) {
@@ -442,15 +446,19 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
           bf16x8_unpack(o, pv);
           const float mean = sum8_dpp(pairs_sum(pv)) * (1.f / 64.f);
           const float m2 = sum8_dpp(pairs_m2(pv, mean));
-          if ((lane & 7) == 7)
-            e.statout[(int64_t)(m_base + p * PR + row) * e.stat_ld + (n_base >> 6)] =
-                float2{mean, m2};
+          if ((lane & 7) == it) stkeep = float2{mean, m2};
         }
       } else {
         float* op = static_cast<float*>(e.out) + idx;
         *reinterpret_cast<f32x4*>(op) = v0;
         *reinterpret_cast<f32x4*>(op + 4) = v1;
       }
+    }
+    if constexpr (OUT_BF16 && STAT && !F8O) {
+      static_assert(NIT <= 8, "one statistics row per lane of an 8-lane group");
+      if ((lane & 7) < NIT)
+        e.statout[(int64_t)(n_base >> 6) * e.stat_ld + m_base + p * PR + (lane & 7) * 8 + rsub] =
+            stkeep;
     }
   }
 }
@@ -801,6 +809,9 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
 #pragma unroll
       for (int i = 0; i < 4; ++i) st[i] = lst[16 * (i0 + i) + fr];
     }
+    // STAT: lanes with fg == i keep row block i's statistics; after the four blocks the 64
+    // lanes hold 64 consecutive rows: one store (slot-major statout plane)
+    [[maybe_unused]] float2 stkeep = float2{0.f, 0.f};
     if constexpr (RPRE) {
       if (i0 == 0) {
         load_raw(4, rraw[1]);
@@ -861,11 +872,11 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
         // squares of the same stored values
         const float mean = xsum32(xsum16(tsum)) * (1.f / 64.f);
         const float m2 = xsum32(xsum16(bf16x8_m2(ob[0], mean) + bf16x8_m2(ob[1], mean)));
-        if (fg == 0)
-          e.statout[(int64_t)(m_base + 16 * (i0 + i) + fr) * e.stat_ld + (n_base >> 6)] =
-              float2{mean, m2};
+        if (fg == i) stkeep = float2{mean, m2};
       }
     }
+    if constexpr (OUT_BF16 && STAT)
+      e.statout[(int64_t)(n_base >> 6) * e.stat_ld + m_base + 16 * (i0 + fg) + fr] = stkeep;
   }
 }
 
@@ -1474,7 +1485,7 @@ bool gemm_emits_stats(int M, int N, int dtype, const vtd_epilogue* e) {
         M % BBM == 0 && N % BBN == 0 && e->bias && e->statout &&
         e->scatter_tokens <= 0 && e->ldo % 8 == 0 && a16(e->out) && a16(e->bias) &&
         (!e->resid || (e->ldr % 8 == 0 && a16(e->resid))) &&
-        (!e->out2 || (e->ldo2 % 8 == 0 && a16(e->out2))) && e->stat_ld >= N / 64 &&
+        (!e->out2 || (e->ldo2 % 8 == 0 && a16(e->out2))) && e->stat_ld >= M &&
         reinterpret_cast<uintptr_t>(e->statout) % 8 == 0))
     return false;
   return (pp2_code(e) & EPI_STAT) != 0 && pp2_code(e) != EPI_GENERIC;

@@ -60,9 +60,9 @@ struct EpiArgs {
   // per column colsum[n] = sum_k Bt[n][k]; acc -> (acc - mean * colsum) * rstd first
   const float2* lnstat; const float* colsum;
   // partial LayerNorm statistics of the stored bf16 rows (fold path producer): per row m
-  // and 64-column block b, statout[m * stat_ld + b] = (block mean, sum of squared
-  // deviations from it) -- centred, so rows with |mean| >> std lose nothing (Chan merge in
-  // ln_stats_finalize_kernel)
+  // and 64-column block b, statout[b * stat_ld + m] = (block mean, sum of squared
+  // deviations from it) -- slot-major planes (a wave's rows of one block are contiguous);
+  // centred, so rows with |mean| >> std lose nothing (Chan merge in ln_stats_finalize_kernel)
   float2* statout; int stat_ld;
   // out_dtype VTD_FP8 (MX-fp8 GEMMs, fast epilogue): e4m3 out + E8M0 scales [n/128][s_rows][4]
   uint8_t* sout; int64_t s_rows;

@@ -459,7 +459,7 @@ __device__ __forceinline__ void w4_epilogue_direct(const f32x4 (&acc)[8][8], int
         const float m2 =
             xsum32(xsum16(bf16x8_m2(ob[2 * b], mean) + bf16x8_m2(ob[2 * b + 1], mean)));
         if (fg == 0)
-          e.statout[(int64_t)mrow * e.stat_ld + (n_base >> 6) + b] = float2{mean, m2};
+          e.statout[(int64_t)((n_base >> 6) + b) * e.stat_ld + mrow] = float2{mean, m2};
       }
     }
   }

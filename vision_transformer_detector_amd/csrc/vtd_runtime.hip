@@ -525,7 +525,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     partials = false;
     // centred per-block partials need every 64-column block full of valid columns
     if (!next_fold || fp8 || dt != VTD_BF16 || !partials_on || D != Dp) return;
-    e.statout = pstat; e.stat_ld = nslot;
+    e.statout = pstat; e.stat_ld = (int)R;       // slot-major planes of R rows
     partials = gemm_emits_stats(M, Dp, dt, &e);
     if (!partials) { e.statout = nullptr; e.stat_ld = 0; }
   };
