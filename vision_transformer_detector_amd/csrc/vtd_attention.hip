@@ -535,7 +535,11 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
 __device__ __forceinline__ int swz_kq(int row) { return (row >> 1) & 7; }
 __device__ __forceinline__ int swz_v(int row) { return ((row >> 1) & 1) << 2; }
 
-template <int NB>   // key blocks of 32: N in (32 (NB - 1), 32 NB]
+// TG: the last key block's 8-key row groups (r >> 2 of a lane's 16 scores) that can hold a key
+// < N, i.e. ceil((N - 32 (NB - 1)) / 8) (4: no trim).  The groups past it hold only masked keys:
+// their exponentials are 0 without being computed, and with TG <= 2 the block's second
+// 16-key PV step (and its V reads) is skipped -- at N = 196 the last block holds 4 keys.
+template <int NB, int TG = 4>   // key blocks of 32: N in (32 (NB - 1), 32 NB]
 __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
     const bf16_t* __restrict__ qkv, int npairs, int N, int heads, int ldqkv, float scale_log2,
     bf16_t* __restrict__ out, int ldo) {
@@ -652,9 +656,11 @@ __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
         va[db] = vl_addr + tr_key * 128 + (((byte >> 4) ^ swv) << 4) + (byte & 15);
       }
       bf16x4 vf[2][2][2][2];                    // [kb parity][st][db][lo / hi]
+      // 16-key PV steps of block kb: 1 for a trimmed last block (TG <= 2)
+      auto nsteps = [](int kb) { return (kb == NB - 1 && TG <= 2) ? 1 : 2; };
       auto vread = [&](int kb, bf16x4 (&f)[2][2][2]) {
 #pragma unroll
-        for (int st = 0; st < 2; ++st)
+        for (int st = 0; st < nsteps(kb); ++st)
 #pragma unroll
           for (int db = 0; db < 2; ++db) {
             const uint32_t a = va[db] + (kb * 32 + 16 * st) * 128;
@@ -673,6 +679,10 @@ __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
           float e[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
+            if (kb == NB - 1 && ((8 * st + j) >> 2) >= TG) {   // only masked keys: exp = 0
+              e[j] = 0.f;
+              continue;
+            }
             e[j] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][8 * st + j], scale_log2, nmx));
             if (j & 1) ps1 += e[j];
             else ps0 += e[j];
@@ -684,13 +694,15 @@ __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
         }
         if (kb + 1 < NB) {
           vread(kb + 1, vf[(kb + 1) & 1]);
-          asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+          // the next block's reads (8, or 4 for a trimmed last block) may stay in flight
+          if (nsteps(kb + 1) == 2) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+          else asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
         } else {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int st = 0; st < 2; ++st)
+        for (int st = 0; st < nsteps(kb); ++st)
 #pragma unroll
           for (int db = 0; db < 2; ++db) {
             const bf16x4 lo = vf[kb & 1][st][db][0], hi = vf[kb & 1][st][db][1];
@@ -994,11 +1006,12 @@ int launch_bf16_ps(const void* qkv, int B, int N, int heads, int ldqkv, float sc
   const int lds = 5 * NR * 128;
   static std::once_flag once[kMaxDevices];
   once_per_device(once, [] {
-    for (const void* f : {reinterpret_cast<const void*>(&attention_bf16_ps_kernel<5>),
-                          reinterpret_cast<const void*>(&attention_bf16_ps_kernel<6>),
-                          reinterpret_cast<const void*>(&attention_bf16_ps_kernel<7>),
-                          reinterpret_cast<const void*>(&attention_bf16_ps_kernel<8>)})
+#define VTD_PS_FN(NB) reinterpret_cast<const void*>(&attention_bf16_ps_kernel<NB, 1>), \
+                      reinterpret_cast<const void*>(&attention_bf16_ps_kernel<NB, 2>), \
+                      reinterpret_cast<const void*>(&attention_bf16_ps_kernel<NB, 4>),
+    for (const void* f : {VTD_PS_FN(5) VTD_PS_FN(6) VTD_PS_FN(7) VTD_PS_FN(8)})
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 5 * 256 * 128);
+#undef VTD_PS_FN
   });
   const int ncu = device_cu_count();
   const int npairs = B * heads;
@@ -1006,10 +1019,15 @@ int launch_bf16_ps(const void* qkv, int B, int N, int heads, int ldqkv, float sc
   // micro-batch streams' attention on disjoint halves of the chip)
   const int kg = knob(VTD_KNOB_ATTN_GRID);
   const int grid = std::min(npairs, kg > 0 ? kg : ncu);
-  auto* kern = NR == 160 ? attention_bf16_ps_kernel<5>
-               : NR == 192 ? attention_bf16_ps_kernel<6>
-               : NR == 224 ? attention_bf16_ps_kernel<7>
-                           : attention_bf16_ps_kernel<8>;
+  // the last block's 8-key groups holding keys < N (1, 2 or 4 = untrimmed)
+  const int tail = N - (NR - 32), tg = tail <= 8 ? 1 : tail <= 16 ? 2 : 4;
+#define VTD_PS_PICK(NB) (tg == 1 ? attention_bf16_ps_kernel<NB, 1>                          \
+                         : tg == 2 ? attention_bf16_ps_kernel<NB, 2> : attention_bf16_ps_kernel<NB, 4>)
+  auto* kern = NR == 160 ? VTD_PS_PICK(5)
+               : NR == 192 ? VTD_PS_PICK(6)
+               : NR == 224 ? VTD_PS_PICK(7)
+                           : VTD_PS_PICK(8);
+#undef VTD_PS_PICK
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, stream, static_cast<const bf16_t*>(qkv),
                      npairs, N, heads, ldqkv, scale * 1.4426950408889634f,
                      static_cast<bf16_t*>(out), ldo);
