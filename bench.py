@@ -415,6 +415,9 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32", "fp8"])
     ap.add_argument("--preset", default="vit_b16_224")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--images", default="letterbox", choices=["letterbox", "uniform"],
+                    help="synthetic inputs: COCO-shaped letterboxed U(-1, 1) images (SURVEY "
+                         "8(d), the default) or plain U(-1, 1) (A/B of the data's effect)")
     ap.add_argument("--no-parity-mode", action="store_true",
                     help="skip the f32 / split-bf16 parity-mode sub-record (headline config only)")
     ap.add_argument("--streams", type=int, default=2,
@@ -454,7 +457,8 @@ def main():
     shape = model.input_shape
     B = args.batch
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
-    images = letterbox_images(B, shape, gen, dev)
+    images = (letterbox_images(B, shape, gen, dev) if args.images == "letterbox"
+              else torch.rand((B,) + tuple(shape), generator=gen, device=dev) * 2 - 1)
 
     from vision_transformer_detector_amd.distributed import all_gather_detections
 
@@ -559,7 +563,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
-        "data": "synthetic (U(-1,1) NHWC letterboxed images generated on device; "
+        "data": ("synthetic (U(-1,1) NHWC letterboxed images generated on device; "
+                 if args.images == "letterbox" else
+                 "synthetic (U(-1,1) NHWC images, no letterbox, generated on device; ") +
                 "random Keras-default-init weights)",
         "config": {"workload": f"{args.preset} detector forward + decode" +
                                (" + RCCL all-gather of detections" if world > 1 else ""),

@@ -749,6 +749,236 @@ __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
 }
 
 // ---------------------------------------------------------------------------------
+// Long-sequence kernel (bf16, DKP = 64, N > 256: C3 N = 1600, C5 N = 576; knob
+// VTD_KNOB_ATTN_VARIANT 6, the default there).  One workgroup = NW waves x 32 queries of one
+// (image, head).  The 64-key chunks of K and V every wave of it reads arrive by LDS-DMA
+// (buffer_load ... lds: no VGPR staging, no staging VALU) into a ring of KS slots of 16 KiB,
+// KS - 1 chunks ahead: per chunk one counted vmcnt (the wave's own pieces of chunk c), one
+// barrier (every piece landed, every wave past chunk c - 1), then the DMA of chunk c + KS - 1
+// into the slot chunk c - 1 used.  The per-chunk arithmetic is attention_bf16_kernel's (scores
+// swapped, S^T = K Q^T; online softmax with the deferred rescale; P^T as the B operand of
+// O^T += V^T P^T) on the persistent kernel's LDS images (128-B rows swizzled on the DMA
+// source, V read by ds_read_b64_tr_b16).  <= 128 VGPRs: 4 waves per SIMD.  NW is picked per N
+// so that the last workgroup of a pair has no idle waves (N = 1600: 5, N = 576: 6).
+template <int CNT>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CNT) : "memory");
+}
+template <int NW, int KS>
+__global__ __launch_bounds__(64 * NW, 4) void attention_bf16_fl_kernel(
+    const bf16_t* __restrict__ qkv, int N, int heads, int ldqkv, float scale_log2,
+    bf16_t* __restrict__ out, int ldo, int nqb) {
+  constexpr int DKP = 64, KC = 64, SLOT = 2 * KC * 128;
+  static_assert(NW >= 4 && NW <= 6 && KS >= 2 && KS <= 4, "fl kernel geometry");
+  typedef __attribute__((address_space(3))) void lds_void_t;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  // wave-uniform in an SGPR: the DMA loop, the counted waits and `active` branch on scalars
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, half = lane >> 5, col = lane & 31;
+  int v = blockIdx.x;                         // XCD-aware: a pair's query blocks share an XCD
+  {
+    const int G = gridDim.x, xcd = v & 7, q8 = G >> 3, r8 = G & 7;
+    v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (v >> 3);
+  }
+  const int pair = v / nqb, qb = v - pair * nqb;
+  const int b = pair / heads, h = pair - b * heads;
+  const int inner = heads * DKP;
+  const int q0 = (qb * NW + wave) * 32;
+  const bool active = q0 < N;
+  const uint32_t lds_base =
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(smem);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(qkv + (int64_t)b * N * ldqkv), 0, N * ldqkv * 2, 0x00020000);
+  const int lrow = lane >> 3, lchunk = lane & 7;
+  const int colk = (inner + h * DKP) * 2, colv = (2 * inner + h * DKP) * 2;
+  // this wave's Q fragments (plain loads: the compiler's wait before their first use also
+  // retires the first chunks' DMA, once)
+  bf16x8 qf[4];
+  {
+    const int q = min(q0 + col, N - 1);
+    const bf16_t* qp = qkv + ((int64_t)b * N + q) * ldqkv + h * DKP;
+#pragma unroll
+    for (int st = 0; st < 4; ++st) qf[st] = *reinterpret_cast<const bf16x8*>(qp + st * 16 + half * 8);
+  }
+  const int nch = (N + KC - 1) / KC;
+  // a chunk = 8 groups of 8 K rows + 8 groups of 8 V rows; wave w issues groups w, w + NW, ..
+  const int my_groups = (8 - wave + NW - 1) / NW;      // 1 or 2
+  auto issue = [&](int c) {
+    char* dst = smem + (c % KS) * SLOT;
+    for (int g = wave; g < 8; g += NW) {
+      const int r = g * 8 + lrow;                       // row within the chunk
+      const int key = min(c * KC + r, N - 1);
+      const int base = key * ldqkv * 2;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + g * 1024), 16,
+                                               base + colk + ((lchunk ^ swz_kq(r)) << 4), 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + KC * 128 + g * 1024), 16,
+                                               base + colv + ((lchunk ^ swz_v(r)) << 4), 0, 0, 0);
+    }
+  };
+  for (int c = 0; c < KS - 1 && c < nch; ++c) issue(c);
+
+  f32x16 o[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+  const int tr_key = 4 * half + ((lane & 15) >> 2);
+  const int tr_byte = ((lane >> 4) & 1) * 32 + (lane & 3) * 8;
+  const int swk = swz_kq(col), swv = swz_v(tr_key);
+  uint32_t va0[2];                                      // V tr-read address in a slot, per db
+#pragma unroll
+  for (int db = 0; db < 2; ++db) {
+    const int byte = db * 64 + tr_byte;
+    va0[db] = KC * 128 + tr_key * 128 + (((byte >> 4) ^ swv) << 4) + (byte & 15);
+  }
+
+  auto chunk = [&](int c, auto last_tag) {
+    constexpr bool LAST = decltype(last_tag)::value;
+    // the wave's pieces of chunk c landed: pieces of the KS - 2 later chunks may fly
+    const int pend = my_groups * 2 * min(KS - 2, nch - 1 - c);
+    switch (pend) {
+      case 0: vm_wait<0>(); break;
+      case 2: vm_wait<2>(); break;
+      case 4: vm_wait<4>(); break;
+      case 6: vm_wait<6>(); break;
+      default: vm_wait<8>(); break;
+    }
+    __builtin_amdgcn_s_barrier();
+    if (!LAST && c + KS - 1 < nch) issue(c + KS - 1);    // into the slot chunk c - 1 used
+    if (!active) return;
+    const char* kl = smem + (c % KS) * SLOT;
+    const uint32_t vs = lds_base + (c % KS) * SLOT;
+    const int kv0 = c * KC;
+    const int nkb = LAST ? min(2, (N - kv0 + 31) >> 5) : 2;
+    const bool ragged = LAST && kv0 + KC > N;
+    f32x16 s[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      if (kb < nkb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+        const char* krow = kl + (kb * 32 + col) * 128;
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+          s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              *reinterpret_cast<const bf16x8*>(krow + (((st * 2 + half) ^ swk) << 4)), qf[st],
+              s[kb], 0, 0, 0);
+      }
+    }
+    if (ragged) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kv0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+          if (key >= N) s[kb][r] = -INFINITY;
+        }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+      if (kb < nkb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
+      }
+    mx = pair_max(mx) * scale_log2;
+    // deferred rescale (attention_bf16_kernel): only when some lane's max grows by > 8
+    if (__builtin_amdgcn_ballot_w64(mx > m_run + 8.f)) {
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+      m_run = m_new;
+      l_run *= alpha;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+    }
+    const float nm = -m_run;
+    float ps0 = 0.f, ps1 = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      if (kb < nkb) {
+        // V^T fragments of this key block (inline asm: see attention_bf16_ps_kernel)
+        bf16x4 vf[2][2][2];
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            const uint32_t a = vs + va0[db] + (kb * 32 + 16 * st) * 128;
+            asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(vf[st][db][0]) : "v"(a));
+            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:1024" : "=v"(vf[st][db][1]) : "v"(a));
+          }
+        bf16x8 pb[2];
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          float e[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            e[j] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][8 * st + j], scale_log2, nm));
+            if (j & 1) ps1 += e[j];
+            else ps0 += e[j];
+          }
+          pb[st] = __builtin_bit_cast(bf16x8, i32x4{(int)pack_bf16x2(e[0], e[1]),
+                                                    (int)pack_bf16x2(e[2], e[3]),
+                                                    (int)pack_bf16x2(e[4], e[5]),
+                                                    (int)pack_bf16x2(e[6], e[7])});
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            const bf16x4 lo = vf[st][db][0], hi = vf[st][db][1];
+            const bf16x8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb[st], o[db], 0, 0, 0);
+          }
+      }
+    }
+    l_run += ps0 + ps1;
+  };
+  for (int c = 0; c + 1 < nch; ++c) chunk(c, std::false_type{});
+  chunk(nch - 1, std::true_type{});
+
+  // every wave done with the ring: O restaged per wave (32 rows x 144 B) and stored as whole
+  // 128-B rows (the buffer range check drops rows >= N)
+  __builtin_amdgcn_s_barrier();
+  const float inv = 1.f / pair_sum(l_run);
+  const uint32_t wst = lds_base + wave * (32 * 144);
+  if (active) {
+    const uint32_t wa = wst + col * 144 + 8 * half;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const uint2 vv = {pack_bf16x2(o[db][4 * g + 0] * inv, o[db][4 * g + 1] * inv),
+                          pack_bf16x2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv)};
+        asm volatile("ds_write_b64 %0, %1 offset:%2" ::"v"(wa), "v"(vv), "n"((db * 32 + 8 * g) * 2)
+                     : "memory");
+      }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+      out + (int64_t)b * N * ldo, 0, N * ldo * 2, 0x00020000);
+  const char* wsp = smem + wave * (32 * 144);
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+    const int r = pass * 8 + lrow;
+    i32x4 vv;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(vv) : "v"(wst + r * 144 + lchunk * 16) : "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (active)
+      __builtin_amdgcn_raw_buffer_store_b128(vv, ro, ((q0 + r) * ldo + h * DKP + lchunk * 8) * 2,
+                                             0, 0);
+  }
+  (void)wsp;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------------
 // Persistent short-sequence kernel, 16 queries per wave (bf16, DKP = 64, N in
 // (16 (NKB - 1), 16 NKB]; the C2 shape N = 196 is NKB = 13).  The 32-query kernel above runs
 // 2 waves per SIMD (7 active of 8 at N = 196) with ~190 registers each: its softmax chains
@@ -1035,6 +1265,42 @@ int launch_bf16_ps(const void* qkv, int B, int N, int heads, int ldqkv, float sc
   return VTD_OK;
 }
 
+// the long-sequence kernel: waves per workgroup chosen so that the last query block of a pair
+// leaves the fewest waves idle (ties: more waves; 4 to 6 -- 8 spills at 128 VGPRs); KS = 3
+// ring slots (48 KiB: 3 workgroups of <= 5 waves per CU, 2 of 6)
+int launch_bf16_fl(const void* qkv, int B, int N, int heads, int ldqkv, float scale, void* out,
+                   int ldo, hipStream_t stream) {
+  constexpr int KS = 3, LDS = KS * 2 * 64 * 128;
+  static std::once_flag once[kMaxDevices];
+  once_per_device(once, [] {
+    for (const void* f : {reinterpret_cast<const void*>(&attention_bf16_fl_kernel<4, KS>),
+                          reinterpret_cast<const void*>(&attention_bf16_fl_kernel<5, KS>),
+                          reinterpret_cast<const void*>(&attention_bf16_fl_kernel<6, KS>)})
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+  });
+  const int nq = (N + 31) / 32;
+  int nw = 6, best = 1 << 30;
+  for (int w : {6, 5, 4}) {
+    const int idle = (nq + w - 1) / w * w - nq;
+    if (idle < best) best = idle, nw = w;
+  }
+  const int nqb = (nq + nw - 1) / nw;
+  VTD_CHECK_ARG((int64_t)nqb * heads * B < INT32_MAX && (int64_t)N * ldqkv * 2 < INT32_MAX &&
+                    (int64_t)N * ldo * 2 < INT32_MAX,
+                "attention: grid / image too large for the long-sequence kernel");
+  const dim3 grid(nqb * heads * B);
+  const float sl2 = scale * 1.4426950408889634f;
+  const bf16_t* q = static_cast<const bf16_t*>(qkv);
+  bf16_t* o = static_cast<bf16_t*>(out);
+  switch (nw) {
+    case 4: hipLaunchKernelGGL((attention_bf16_fl_kernel<4, KS>), grid, dim3(256), LDS, stream, q, N, heads, ldqkv, sl2, o, ldo, nqb); break;
+    case 5: hipLaunchKernelGGL((attention_bf16_fl_kernel<5, KS>), grid, dim3(320), LDS, stream, q, N, heads, ldqkv, sl2, o, ldo, nqb); break;
+    default: hipLaunchKernelGGL((attention_bf16_fl_kernel<6, KS>), grid, dim3(384), LDS, stream, q, N, heads, ldqkv, sl2, o, ldo, nqb);
+  }
+  VTD_LAUNCH_CHECK("attention_bf16_fl");
+  return VTD_OK;
+}
+
 template <int DKP, int NWG, bool MX8 = false>
 int launch_bf16_v2(const void* qkv, int B, int N, int heads, int ldqkv, float scale,
                    void* out, int ldo, hipStream_t stream, uint8_t* s8 = nullptr,
@@ -1111,6 +1377,10 @@ int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqk
 #endif
     if ((v1 == 4 || v1 == 5) && ps_ok)
       return launch_bf16_ps(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+    // 6: the long-sequence LDS-DMA kernel (dkp 64, N > 256; knob value 6 forces it for any
+    // N, e.g. tests); with the default (4) it serves dkp 64, N > 256
+    if (dkp == 64 && ldqkv % 8 == 0 && ldo % 8 == 0 && (v1 == 6 || (v1 == 4 && N > 256)))
+      return launch_bf16_fl(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
     if (v1 == 1) {
       if (dkp == 32) return launch<bf16_t, 32>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
       if (dkp == 64) return launch<bf16_t, 64>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
