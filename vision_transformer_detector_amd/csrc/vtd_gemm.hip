@@ -298,13 +298,10 @@ __device__ __forceinline__ void store_s3(const EpiArgs& e, int64_t idx, const i3
 }
 // TRL: the accumulators are in the transposed layout (lane (fr, fg): row 16 i + fr, columns
 // 32 jp + 8 fg .. + 7 in acc[i][2 jp], acc[i][2 jp + 1]): staged with ds_write_b128
-// RL: the residual rows of the first pass were prefetched into LDS at rl (the wave's 4 KiB,
-// lane-linear: 16 B of iteration it at rl + it * 1024 + lane * 16) by the K loop's last step
-template <int EPI, int PR = 32, int DG = 0, typename PF = NoPF, bool TRL = false, bool RL = false>
+template <int EPI, int PR = 32, int DG = 0, typename PF = NoPF, bool TRL = false>
 __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* ep, int lane,
                                               int m_base, int n_base, const EpiArgs& e,
-                                              const float2* lst = nullptr, PF pf = PF{},
-                                              const char* rl = nullptr) {
+                                              const float2* lst = nullptr, PF pf = PF{}) {
   constexpr int ACT = EPI & 3;
   constexpr bool OUT_BF16 = (EPI & 4) != 0;
   constexpr bool RESID = (EPI & 8) != 0 && !(DG & 2);
@@ -343,17 +340,8 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
                                                 n_base + c8);
     }
   };
-  if constexpr (RPRE && RL) {
-    static_assert(PR == 32, "the residual prefetch covers one 32-row pass");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // the wave's own LDS-DMA landed
-#pragma unroll
-    for (int it = 0; it < NIT; ++it)
-      rraw[0][it] = *reinterpret_cast<const i32x4*>(rl + it * 1024 + lane * 16);
-  } else if constexpr (RPRE) {
-    load_raw(0, rraw[0]);
-  } else {
-    pf();
-  }
+  if constexpr (RPRE) load_raw(0, rraw[0]);
+  else pf();
 #pragma unroll
   for (int p = 0; p < 128 / PR; ++p) {
     if constexpr (TRL) {
@@ -695,14 +683,10 @@ __device__ __forceinline__ void pp2_issue(char* smem, const PP2BufSrc& src, int 
 // before K-tile 1 is loaded over it.
 // NB (diagnostic build, VTD_PP2_DG & 32, wrong outputs): the K loop's per-phase barriers
 // dropped -- the cost of the ping-pong synchronisation itself
-// LF (last-step prefetch): issued in the last K-step once its first wait has retired every
-// K-tile DMA, so the step's later waits can let it fly (LFN = its vector-memory instructions
-// per wave); the epilogue's first residual rows (pp2 kernel, residual layers)
-template <bool TR, bool F32 = false, bool NB = false, typename LF = NoPF, int LFN = 0>
+template <bool TR, bool F32 = false, bool NB = false>
 __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, const PP2BufSrc& src,
                                              int nk, int wave, int wm, int wn, int fr, int fg,
-                                             uint64_t* t_prologue = nullptr, bool pre = false,
-                                             LF lf = LF{}) {
+                                             uint64_t* t_prologue = nullptr, bool pre = false) {
   // prologue: tile 0 complete, tile 1's X0/Y0/Y1 in flight
   if (!pre) {
     pp2_issue<0>(smem, src, wave, 0, 0);
@@ -737,7 +721,6 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
     if constexpr (n1) pp2_issue<1>(smem, src, wave, kt + 1, (kt + 1) & 1);
     if constexpr (n1) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if constexpr (!n1 && !n2) lf();            // the last step: every K-tile has landed
     if constexpr (!NB) pp_barrier();
     if constexpr (TR) pp_mfma_t<0, 0, F32>(acc, a, b0);
     else pp_mfma<0, 0, F32>(acc, a, b0);
@@ -746,7 +729,7 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
     if constexpr (TR) pp_load_b_t(b1, st + 3 * 16384, rb, fr, fg);
     else pp_load_b(b1, st + 3 * 16384, rb, fr, fg);
     if constexpr (n1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if constexpr (n2 || LFN == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (!NB) pp_barrier();
     if constexpr (TR) pp_mfma_t<0, 2, F32>(acc, a, b1);
     else pp_mfma<0, 2, F32>(acc, a, b1);
@@ -763,7 +746,7 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
       pp2_issue<2>(smem, src, wave, kt + 2, kt & 1);
       pp2_issue<3>(smem, src, wave, kt + 2, kt & 1);
       asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-    } else if constexpr (n1 || LFN == 0) {
+    } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     if constexpr (!NB) pp_barrier();
@@ -971,27 +954,8 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
     ts[0] = __builtin_amdgcn_s_memtime();
     rt0 = __builtin_amdgcn_s_memrealtime();
   }
-  // residual layers on the LDS-staged epilogue (bf16 stream, full tiles): the first pass's
-  // residual rows arrive by LDS-DMA during the last K-step, into the 32 KiB past the stages
-  constexpr bool RLDS = !TR && EPI != EPI_GENERIC && (EPI & 12) == 12 && (EPI & EPI_F8O) == 0 &&
-                        (EPI & EPI_PARTIAL) == 0 && (DG & 2) == 0;
-  const bool full_tile = m0 + BBM <= M && n0 + BBN <= N;
-  char* const rlds = smem + 2 * BSTAGE + wave * 4096;
-  auto rpf = [&]() {
-    if constexpr (RLDS) {
-      if (full_tile) {
-        const int rsub = lane >> 3, c8 = (lane & 7) * 8;
-        const bf16_t* rp = static_cast<const bf16_t*>(e.resid) +
-                           (int64_t)(m0 + wm * 128 + rsub) * e.ldr + n0 + wn * 64 + c8;
-#pragma unroll
-        for (int it = 0; it < 4; ++it)
-          __builtin_amdgcn_global_load_lds((gbl_void_t*)(rp + (int64_t)it * 8 * e.ldr),
-                                           (lds_void_t*)(rlds + it * 1024), 16, 0, 0);
-      }
-    }
-  };
-  pp2_mainloop<TR, false, (DG & 32) != 0, decltype(rpf), RLDS ? 4 : 0>(
-      acc, smem, src, nk, wave, wm, wn, fr, fg, (DG & 16) ? &ts[1] : nullptr, false, rpf);
+  pp2_mainloop<TR, false, (DG & 32) != 0>(acc, smem, src, nk, wave, wm, wn, fr, fg,
+                                           (DG & 16) ? &ts[1] : nullptr);
   if constexpr ((DG & 16) != 0) ts[2] = __builtin_amdgcn_s_memtime();
   const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
 #if VTD_DIAG
@@ -1049,9 +1013,8 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
   }
   float* ep = reinterpret_cast<float*>(smem) + wave * 32 * 68;
   if constexpr (EPI != EPI_GENERIC) {
-    if (full_tile) {
-      epilogue_fast<EPI, 32, DG, NoPF, false, RLDS>(acc, ep, lane, m_base, n_base, e, lds_st,
-                                                    NoPF{}, rlds);
+    if (m0 + BBM <= M && n0 + BBN <= N) {
+      epilogue_fast<EPI, 32, DG>(acc, ep, lane, m_base, n_base, e, lds_st);
       stamp();
       return;
     }
@@ -1563,16 +1526,6 @@ constexpr bool pp2_mt_code(int c) {
 // tiles per pp2 workgroup (knob VTD_KNOB_GEMM_TPW)
 inline int pp2_tpw() { return std::max(1, knob(VTD_KNOB_GEMM_TPW)); }
 
-// dynamic LDS of a pp2 instantiation: the two stages, plus 32 KiB for the first pass's
-// residual rows on the LDS-staged residual codes (kernel: RLDS)
-constexpr size_t pp2_lds(int C, bool tr) {
-  return (!tr && C != EPI_GENERIC && (C & 12) == 12 && (C & EPI_F8O) == 0 &&
-          (C & EPI_PARTIAL) == 0)
-             ? 2 * BSTAGE + 8 * 4096
-             : 2 * BSTAGE;
-}
-static_assert(2 * BSTAGE + 8 * 4096 <= 160 * 1024, "pp2 residual prefetch LDS");
-
 template <int C>
 void pp2_launch(bool tr, dim3 g, hipStream_t stream, int M, int N, int K, const bf16_t* A, int lda,
                 const bf16_t* Bt, int ldb, int tiles_m, int tiles_n, const EpiArgs& e,
@@ -1592,11 +1545,11 @@ void pp2_launch(bool tr, dim3 g, hipStream_t stream, int M, int N, int K, const 
   }
 #endif
   if (tr)
-    hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, true>), g, dim3(BNT), pp2_lds(C, true), stream,
-                       M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e, ksplit);
+    hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, true>), g, dim3(BNT), 2 * BSTAGE, stream, M,
+                       N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e, ksplit);
   else
-    hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, false>), g, dim3(BNT), pp2_lds(C, false),
-                       stream, M, N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e, ksplit);
+    hipLaunchKernelGGL((gemm_tn_bf16_pp2_kernel<C, false>), g, dim3(BNT), 2 * BSTAGE, stream, M,
+                       N, K, A, lda, Bt, ldb, tiles_m, tiles_n, e, ksplit);
 }
 
 void pp2_set_attributes() {
@@ -1607,8 +1560,7 @@ void pp2_set_attributes() {
     const void* fns[] = {VTD_PP_FN(EPI_GENERIC) VTD_PP2_CODES(VTD_PP_FN)};
 #undef VTD_PP_FN
     for (const void* f : fns)
-      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(2 * BSTAGE + 8 * 4096));
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BSTAGE);
 #if VTD_DIAG
 #define VTD_MT_FN(C) reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_mt_kernel<C, false>), \
                      reinterpret_cast<const void*>(&gemm_tn_bf16_pp2_mt_kernel<C, true>),
