@@ -297,7 +297,7 @@ def test_attention_persistent_equals_per_pair_kernel(L, cuda, monkeypatch, B, N,
 
 @pytest.mark.parametrize("B,N,H", [(4, 1600, 12), (6, 576, 16), (3, 1100, 5), (2, 300, 3)])
 def test_attention_long_sequence_equals_streaming_kernel(L, cuda, B, N, H):
-    """The long-sequence LDS-DMA kernel (knob 6; the default for dkp 64, N > 256) against the
+    """The long-sequence LDS-DMA kernel (knob 6, opt-in) against the
     register-staged streaming kernel (knob 2) at the C3 / C5 shapes and ragged ones: the same
     64-key chunks and deferred-rescale online softmax, so equal to within bf16 rounding of P
     (both against fp64 in test_attention)."""

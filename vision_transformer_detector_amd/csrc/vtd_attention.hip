@@ -749,8 +749,9 @@ __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
 }
 
 // ---------------------------------------------------------------------------------
-// Long-sequence kernel (bf16, DKP = 64, N > 256: C3 N = 1600, C5 N = 576; knob
-// VTD_KNOB_ATTN_VARIANT 6, the default there).  One workgroup = NW waves x 32 queries of one
+// Long-sequence kernel (bf16, DKP = 64, N > 256: C3 N = 1600, C5 N = 576; opt-in, knob
+// VTD_KNOB_ATTN_VARIANT 6: measured 12 % / 5 % SLOWER than the streaming kernel at C3 / C5,
+// profiles/r05_attn_fl_ab.log -- kept for the record and for its tests).  One workgroup = NW waves x 32 queries of one
 // (image, head).  The 64-key chunks of K and V every wave of it reads arrive by LDS-DMA
 // (buffer_load ... lds: no VGPR staging, no staging VALU) into a ring of KS slots of 16 KiB,
 // KS - 1 chunks ahead: per chunk one counted vmcnt (the wave's own pieces of chunk c), one
@@ -1377,9 +1378,9 @@ int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqk
 #endif
     if ((v1 == 4 || v1 == 5) && ps_ok)
       return launch_bf16_ps(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
-    // 6: the long-sequence LDS-DMA kernel (dkp 64, N > 256; knob value 6 forces it for any
-    // N, e.g. tests); with the default (4) it serves dkp 64, N > 256
-    if (dkp == 64 && ldqkv % 8 == 0 && ldo % 8 == 0 && (v1 == 6 || (v1 == 4 && N > 256)))
+    // 6: the long-sequence LDS-DMA kernel (dkp 64, any N; opt-in: measured slower than the
+    // streaming kernel at C3 / C5, profiles/r05_attn_fl_ab.log)
+    if (dkp == 64 && ldqkv % 8 == 0 && ldo % 8 == 0 && v1 == 6)
       return launch_bf16_fl(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
     if (v1 == 1) {
       if (dkp == 32) return launch<bf16_t, 32>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
