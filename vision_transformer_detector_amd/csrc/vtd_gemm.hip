@@ -240,6 +240,13 @@ constexpr int BBM = 256, BBN = 256, BNT = 512;
 #ifndef VTD_TRS
 #define VTD_TRS 0
 #endif
+// K-loop phases per K-step of the bf16 256 x 256 kernel: 2 (pp2_mainloop_2ph, the default:
+// C2 forward +1.6-2.2 %, mlp1 -5 %, head2 -6.5 %, profiles/r05_pp2_2phase_ab.log) or 4
+// (pp2_mainloop; -DVTD_PP2_PH=4 A/B builds).  The f32 and MX-fp8 kernels keep four phases
+// (two measured -1.1 % / -0.3 %).
+#ifndef VTD_PP2_PH
+#define VTD_PP2_PH 2
+#endif
 constexpr int BSTAGE = (BBM + BBN) * KB;     // 64 KiB per stage
 static_assert(8 * 32 * 68 * 4 + 8 * 128 * 8 <= 2 * BSTAGE,
               "epilogue staging + LayerNorm-fold row tables must fit the stages");
@@ -761,6 +768,95 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
   if (wm == 0) pp_barrier();                 // re-align
 }
 
+// 32-MFMA cluster: row blocks I0..I0+3 against all four column blocks
+template <int I0, bool TR, bool F32>
+__device__ __forceinline__ void pp_mfma32(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][2],
+                                          const bf16x8 (&b0)[2][2], const bf16x8 (&b1)[2][2]) {
+  if constexpr (TR) {
+    pp_mfma_t<I0, 0, F32>(acc, a, b0);
+    pp_mfma_t<I0, 2, F32>(acc, a, b1);
+  } else {
+    pp_mfma<I0, 0, F32>(acc, a, b0);
+    pp_mfma<I0, 2, F32>(acc, a, b1);
+  }
+}
+
+// Two-phase K-step (the same stages, DMA groups and LDS image as pp2_mainloop): phase X
+// reads A quad X0 and both B quads and runs row blocks 0-3 x all columns (32 MFMAs), phase Y
+// reads A quad X1 and runs row blocks 4-7 -- four barriers per K-step instead of eight.
+// Windows (e = workgroup barrier events, G1 one event behind G0): G0 reads X(t) in
+// (4t-1, 4t), Y(t) in (4t+1, 4t+2); G1 in (4t, 4t+1), (4t+2, 4t+3).
+//   X(t): DMA X1(t+1)         -> stage (t+1)&1 | wait vmcnt(8): X1(t) landed
+//   Y(t): DMA X0,Y0,Y1(t+2)   -> stage t&1     | wait vmcnt(8): X0,Y0,Y1(t+1) landed
+// WAR: X1(t+1) overwrites X1(t-1), whose last reads (G1, Y(t-1)) retired by 4t-1; the X(t)
+// windows open at 4t-1 (G0) / 4t (G1).  X0,Y0,Y1(t+2) overwrite tile t's, last read by G1 in
+// X(t), retired by 4t+1; the Y(t) windows open at 4t+1 / 4t+2.  RAW: every wave waits for its
+// own DMA before the barrier that opens the readers' window.
+template <bool TR, bool F32 = false>
+__device__ __forceinline__ void pp2_mainloop_2ph(f32x4 (&acc)[8][4], char* smem,
+                                                 const PP2BufSrc& src, int nk, int wave, int wm,
+                                                 int wn, int fr, int fg,
+                                                 uint64_t* t_prologue = nullptr) {
+  // prologue: X0,Y0,Y1,X1(0) complete; X0,Y0,Y1(1) in flight
+  pp2_issue<0>(smem, src, wave, 0, 0);
+  pp2_issue<2>(smem, src, wave, 0, 0);
+  pp2_issue<3>(smem, src, wave, 0, 0);
+  pp2_issue<1>(smem, src, wave, 0, 0);
+  if (nk > 1) {
+    pp2_issue<0>(smem, src, wave, 1, 1);
+    pp2_issue<2>(smem, src, wave, 1, 1);
+    pp2_issue<3>(smem, src, wave, 1, 1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  pp_barrier();
+  if (t_prologue) *t_prologue = __builtin_amdgcn_s_memtime();   // diagnostic stamps only
+  if (wm == 1) pp_barrier();                 // stagger G1 by one barrier
+  const int ra = wm * 64, rb = wn * 32;
+  bf16x8 a[4][2], b0[2][2], b1[2][2];
+  auto step = [&](int kt, auto t1, auto t2) {
+    const char* st = smem + (kt & 1) * BSTAGE;
+    constexpr bool n1 = decltype(t1)::value, n2 = decltype(t2)::value;
+    // ---- X
+    pp_load_a(a, st + 0 * 16384, ra, fr, fg);
+    if constexpr (TR) {
+      pp_load_b_t(b0, st + 2 * 16384, rb, fr, fg);
+      pp_load_b_t(b1, st + 3 * 16384, rb, fr, fg);
+    } else {
+      pp_load_b(b0, st + 2 * 16384, rb, fr, fg);
+      pp_load_b(b1, st + 3 * 16384, rb, fr, fg);
+    }
+    if constexpr (n1) {
+      pp2_issue<1>(smem, src, wave, kt + 1, (kt + 1) & 1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    pp_barrier();
+    pp_mfma32<0, TR, F32>(acc, a, b0, b1);
+    pp_barrier();
+    // ---- Y
+    pp_load_a(a, st + 1 * 16384, ra, fr, fg);
+    if constexpr (n2) {
+      pp2_issue<0>(smem, src, wave, kt + 2, kt & 1);
+      pp2_issue<2>(smem, src, wave, kt + 2, kt & 1);
+      pp2_issue<3>(smem, src, wave, kt + 2, kt & 1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    pp_barrier();
+    pp_mfma32<4, TR, F32>(acc, a, b0, b1);
+    pp_barrier();
+  };
+  int kt = 0;
+  for (; kt + 2 < nk; ++kt) step(kt, std::true_type{}, std::true_type{});
+  if (kt + 1 < nk) step(kt++, std::true_type{}, std::false_type{});
+  step(kt, std::false_type{}, std::false_type{});
+  if (wm == 0) pp_barrier();                 // re-align
+}
+
 // Epilogue of the transposed variant, full tiles: lane (fr, fg) of wave (wm, wn) holds,
 // for accumulator row block i and column half jp, output row m_base + 16 i + fr and the 8
 // contiguous columns n_base + 32 jp + 8 fg + 0..7 (acc[i][2 jp] = first 4, acc[i][2 jp + 1]
@@ -954,8 +1050,11 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
     ts[0] = __builtin_amdgcn_s_memtime();
     rt0 = __builtin_amdgcn_s_memrealtime();
   }
-  pp2_mainloop<TR, false, (DG & 32) != 0>(acc, smem, src, nk, wave, wm, wn, fr, fg,
-                                           (DG & 16) ? &ts[1] : nullptr);
+  if constexpr (VTD_PP2_PH == 2 && (DG & 32) == 0)
+    pp2_mainloop_2ph<TR>(acc, smem, src, nk, wave, wm, wn, fr, fg, (DG & 16) ? &ts[1] : nullptr);
+  else
+    pp2_mainloop<TR, false, (DG & 32) != 0>(acc, smem, src, nk, wave, wm, wn, fr, fg,
+                                             (DG & 16) ? &ts[1] : nullptr);
   if constexpr ((DG & 16) != 0) ts[2] = __builtin_amdgcn_s_memtime();
   const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
 #if VTD_DIAG
@@ -1178,6 +1277,8 @@ __global__ __launch_bounds__(BNT) void gemm_tn_f32_pp2_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fg = lane >> 4;
+  // four phases: with four f32 MFMAs per fragment pair the clusters are long enough (the
+  // two-phase step measured -1.1 %, profiles/r05_pp2_2phase_ab.log)
   pp2_mainloop<TR, true>(acc, smem, src, K / 32, wave, wm, wn, fr, fg);
   const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
   if constexpr (TR) {
