@@ -844,17 +844,20 @@ __device__ __forceinline__ void pp2_mainloop_2ph(f32x4 (&acc)[8][4], char* smem,
       pp2_issue<3>(smem, src, wave, kt + 2, kt & 1);
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // last K-step: every LDS read retired before the barrier, so that G0, released
+      // into its epilogue by the next one, cannot overwrite a stage G1 is still reading
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
     pp_barrier();
     pp_mfma32<4, TR, F32>(acc, a, b0, b1);
-    pp_barrier();
+    // the last Y-phase barrier is G0's alone (G1's Y-phase barrier above): G0's epilogue then
+    // runs beside G1's last MFMA cluster instead of waiting for it (no re-align barrier)
+    if (n1 || n2 || wm == 0) pp_barrier();
   };
   int kt = 0;
   for (; kt + 2 < nk; ++kt) step(kt, std::true_type{}, std::true_type{});
   if (kt + 1 < nk) step(kt++, std::true_type{}, std::false_type{});
   step(kt, std::false_type{}, std::false_type{});
-  if (wm == 0) pp_barrier();                 // re-align
 }
 
 // Epilogue of the transposed variant, full tiles: lane (fr, fg) of wave (wm, wn) holds,
