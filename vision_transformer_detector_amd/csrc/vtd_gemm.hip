@@ -1022,6 +1022,10 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
   const int wm = wave >> 2, wn = wave & 3;
   const int nt = tiles_m * tiles_n, nwg = nt * ksplit;
   const int bid = blockIdx.x;
+#if VTD_DIAG
+  if (e.dsl > 0 && bid < 256 && ((bid >> 3) & 1))
+    for (int i = 0; i < e.dsl; ++i) __builtin_amdgcn_s_sleep(8);
+#endif
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int v = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   // one K range (the forward's launches): no division by the tile count or split count
@@ -1805,6 +1809,10 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
     e.ngw = ngw;
     e.to = make_tile_order(tiles_m, tiles_n, e.ngw);
     e.tpw = VTD_DIAG ? pp2_tpw() : 1;   // several tiles per workgroup: diagnostic build only
+#if VTD_DIAG
+    static const int pp2_sleep = getenv("VTD_PP2_SLEEP") ? atoi(getenv("VTD_PP2_SLEEP")) : 0;
+    e.dsl = pp2_sleep;
+#endif
     const int code = pp2_code(epi);
     // transposed accumulators + register-direct epilogue for activation layers (mlp1 -5 %,
     // mlp2 -1.5 %), LDS-staged row vectors for the others (attn_out -10 %, mlp3 -4 %);

@@ -84,6 +84,9 @@ struct EpiArgs {
   TileOrder to;
   // out_dtype VTD_BF16X3: width of one piece of the split-bf16 output row (ldo / 3)
   int s3;
+  // diagnostic build only (VTD_PP2_SLEEP): first-round pp2 workgroups in odd XCD slots start
+  // dsl x 512 cycles late (epilogue phases of neighbouring CUs out of step); 0 in the product
+  int dsl;
 };
 
 // bf16 output row vector store of the fast epilogues; build-time A/B knob VTD_OUT_NT: 1 =
