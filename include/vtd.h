@@ -447,7 +447,8 @@ int vtd_profile_read(double* ms, int64_t* launches, double* flops, int n_classes
  *   VTD_KNOB_F32_PP2 (VTD_F32_PP2): 0 keeps large fp32-mode GEMMs on the 128 x 128 kernel
  *     instead of the 256-tile f32 one.
  *   VTD_KNOB_STAGGER (VTD_STAGGER): the two-stream split's second micro-batch starts k stages
- *     (patch embedding, encoder layers) behind the first (default 0: in phase).
+ *     (patch embedding, encoder layers) behind the first (default: 1 for parts of at most 32
+ *     row tiles of 256 -- C2 at B = 64 -- else 0, in phase).
  *   VTD_KNOB_GEMM_TR (VTD_GEMM_TR): 256-tile bf16 GEMM accumulator layout, 1 = transposed
  *     (register-direct epilogue) for every layer, 0 = for none (default: activation layers).
  *   VTD_KNOB_FIN_WGS (VTD_FIN_WGS): LayerNorm-statistics finalize as n grid-stride

@@ -1536,7 +1536,18 @@ int gemm_variant() {
 
 // Fewest 256 x 256 tiles for which the bf16 path takes the 256-tile kernels (below: the
 // 128 x 128 gemm_tn_kernel; measured within noise from 1 to 128 tiles on the head's GEMMs).
-constexpr int kMinBigTiles = 128;
+// 64 since round 5: the N = 768 layers of C2 at B = 64 in two parts (75 tiles each) ran the
+// 128 x 128 kernel at 161 us per launch against 27-43 us for the whole batch on pp2
+// (profiles/r05_b64_split_trace_*.txt); with 64 the split B = 64 forward is +15 %
+// (profiles/r05_b64_split_ab.log).  VTD_MIN_BIG_TILES overrides (A/B).
+int min_big_tiles() {
+  static const int t = [] {
+    const char* v = getenv("VTD_MIN_BIG_TILES");
+    return v ? std::max(1, atoi(v)) : 64;
+  }();
+  return t;
+}
+#define kMinBigTiles min_big_tiles()
 
 // pp2 / w4 tile order: weight-panel groups of 4 n-tiles (3 at 6) walked down the m-rows keep
 // an XCD's B panels in its L2 (measured per shape, round 2: qkv / mlp1 / head1 -3.3..-4 %,

@@ -228,7 +228,23 @@ int resid_dtype(int dtype) {
   return act_dtype(dtype) == VTD_BF16 && !f32 ? VTD_BF16 : VTD_F32;
 }
 int k8_of(int k) { return (int)round_up(k, 128); }
-Plan make_plan(const vtd_config* c, const vtd_dims& d) {
+// Encoder rows of a micro-batch part: a part's batch x tokens rounded up to whole 256-row
+// tiles (pad), so that every encoder GEMM of the part runs full tiles -- the fast epilogues
+// and the producer-side LayerNorm partial statistics -- instead of a last partial row tile
+// on the generic epilogue (C2 at B = 64 in two parts of 32 images: 6272 rows -> 6400).  The
+// pad rows start from zero patches; rows never mix in a GEMM, LayerNorm or the attention
+// (which reads the real images' rows only), and the head reads the real rows only.
+int64_t gemm_rows(const vtd_dims& d, bool pad) { return pad ? round_up(d.rows, 256) : d.rows; }
+// whether the parts of a split forward pad their rows (VTD_SPLIT_PAD=0: not, A/B only)
+bool split_pad() {
+  static const bool on = [] {
+    const char* v = getenv("VTD_SPLIT_PAD");
+    return !v || atoi(v) != 0;
+  }();
+  return on;
+}
+// pad: the encoder runs on rows rounded up to whole 256-row GEMM tiles (gemm_rows)
+Plan make_plan(const vtd_config* c, const vtd_dims& d, bool pad = false) {
   Plan p{};
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -237,7 +253,7 @@ Plan make_plan(const vtd_config* c, const vtd_dims& d) {
     return o;
   };
   const size_t es = es_of(c->dtype), eop = eop_of(c->dtype);
-  const size_t R = (size_t)d.rows, HR = (size_t)d.head_rows;
+  const size_t R = (size_t)gemm_rows(d, pad), HR = (size_t)d.head_rows;
   int mlp_max = 0, head_max = 0;
   for (int j = 0; j < c->mlp_quantities; ++j) mlp_max = std::max(mlp_max, d.mlp_units_p[j]);
   for (int j = 0; j < d.n_head; ++j) head_max = std::max(head_max, d.head_units_p[j]);
@@ -286,11 +302,13 @@ Plan make_plan(const vtd_config* c, const vtd_dims& d) {
 // instead of leaving CUs idle.  VTD_STREAMS=1 disables it; so does per-kernel profiling
 // (vtd_profile_enable): each profiled launch then runs alone and its events time it.
 constexpr int kMaxSplit = 4;   // VTD_STREAMS is clamped to [1, kMaxSplit]
-// fewest 256-row tiles per part (VTD_SPLIT_MIN_TILES; C2 at B = 256, 2 parts: 98 each)
+// fewest 256-row tiles per part (VTD_SPLIT_MIN_TILES; C2 at B = 256, 2 parts: 98 each; at
+// B = 64, 2 parts of 24.5 tiles padded to 25: +15 % over one stream since round 5, once the
+// parts' 75-tile layers run the 256-tile kernels, profiles/r05_b64_split_ab.log)
 int split_min_tiles() {
   static const int t = [] {
     const char* v = getenv("VTD_SPLIT_MIN_TILES");
-    return v ? std::max(1, atoi(v)) : 48;
+    return v ? std::max(1, atoi(v)) : 24;
   }();
   return t;
 }
@@ -324,7 +342,7 @@ size_t split_workspace(const vtd_config* c, const vtd_dims& d) {
     const vtd_config sc = sub_config(c, i, ns);
     vtd_dims sd;
     if (derive(&sc, &sd) != VTD_OK) return 0;
-    total += make_plan(&sc, sd).total;
+    total += make_plan(&sc, sd, split_pad()).total;
   }
   return std::max(total, whole);
 }
@@ -368,7 +386,7 @@ SideStream* side_stream(hipStream_t st) {
 // "the GEMM that last wrote x emitted LayerNorm partials" from one stage to the next.
 int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* images,
                  float* logits, float* dets, char* ws, hipStream_t st, int s_lo, int s_hi,
-                 bool& partials);
+                 bool& partials, bool pad);
 }  // namespace
 
 }  // namespace vtd
@@ -420,7 +438,8 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
   const int n_stages = cfg->repeat_times + 2;
   if (!side) {
     bool partials = false;
-    if (ns == 1) return forward_impl(cfg, w, images, logits, dets, ws, st, 0, n_stages, partials);
+    if (ns == 1)
+      return forward_impl(cfg, w, images, logits, dets, ws, st, 0, n_stages, partials, false);
     // no side stream (first call under capture): the halves run in order on `st`
   }
   const size_t img = (size_t)cfg->image_h * cfg->image_w * cfg->channels;
@@ -430,7 +449,12 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
   // fork: one record, every side stream waits on it.  Knob VTD_KNOB_STAGGER = k > 0: the
   // record follows the caller-stream part's first k stages, so the other parts run k
   // stages behind (their kernels then pair with different kernels of the first part)
-  const int stagger = side ? std::min(std::max(knob(VTD_KNOB_STAGGER), 0), n_stages) : 0;
+  // default: one stage behind for small parts (<= 32 row tiles: C2 at B = 64, +1.5 %), in
+  // phase otherwise (B = 96 / 128 / 256: 0 to -1.5 % with a stagger; profiles/r05_b64_split_ab.log)
+  const int ks = knob(VTD_KNOB_STAGGER);
+  const int part_tiles = (int)((d.rows / ns + 255) / 256);
+  const int stagger =
+      side ? std::min(ks >= 0 ? ks : (part_tiles <= 32 ? 1 : 0), n_stages) : 0;
   auto fork = [&]() -> int {
     VTD_HIP(hipEventRecord(side->fork, st));
     for (int part = 1; part < ns; ++part) VTD_HIP(hipStreamWaitEvent(side->s[part - 1], side->fork, 0));
@@ -462,7 +486,7 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
     P.ws = ws + ws_off;
     P.partials = false;
     b0 += P.cfg.batch;
-    ws_off += make_plan(&P.cfg, dp).total;
+    ws_off += make_plan(&P.cfg, dp, split_pad()).total;
   }
   // Launches are interleaved part by part, one stage (encoder layer) at a time: issuing
   // all of one part's ~110 launches before the next part's first one left the second
@@ -475,7 +499,8 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
       Part& P = parts[part];
       const int s = part == 0 ? t : t - stagger;
       if (s < 0 || s >= n_stages) continue;
-      rc = forward_impl(&P.cfg, w, P.images, P.logits, P.dets, P.ws, P.st, s, s + 1, P.partials);
+      rc = forward_impl(&P.cfg, w, P.images, P.logits, P.dets, P.ws, P.st, s, s + 1, P.partials,
+                        split_pad());
       if (rc) return rc;
     }
   }
@@ -493,11 +518,11 @@ namespace vtd {
 namespace {
 int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* images,
                  float* logits, float* dets, char* ws, hipStream_t st, int s_lo, int s_hi,
-                 bool& partials) {
+                 bool& partials, bool pad) {
   vtd_dims d;
   int rc = derive(cfg, &d);
   if (rc) return rc;
-  const Plan P = make_plan(cfg, d);
+  const Plan P = make_plan(cfg, d, pad);
   const bool fp8 = cfg->dtype == VTD_FP8;
   const int dt = act_dtype(cfg->dtype);
   // VTD_BF16X3: every GEMM runs on split-bf16 operands (bf16 kernels over K' = 3 K_p), whose
@@ -506,7 +531,8 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   const int gdt = x3 ? VTD_BF16 : dt, odt = x3 ? VTD_BF16X3 : dt;
   auto kk = [&](int k) { return opk(cfg->dtype, k); };
   const int B = cfg->batch, N = d.tokens, D = d.d, Dp = d.d_p;
-  const int64_t R = d.rows;
+  // R: the encoder's rows (the real batch x tokens, or whole 256-row tiles of a part: pad)
+  const int64_t R = gemm_rows(d, pad);
   VTD_CHECK_ARG(R < (int64_t)1 << 31, "forward: batch*tokens too large");
   const int M = (int)R;
   void* patches = ws + P.patches;
@@ -553,7 +579,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   void* u = ws + P.u;
   void* head[2] = {ws + P.head0, ws + P.head1};
   const int act = cfg->use_mish ? VTD_ACT_MISH : VTD_ACT_GELU_TANH;
-  const double fR = (double)R;
+  const double fR = (double)d.rows;             // algorithmic FLOPs: the real rows
   uint8_t* q8 = reinterpret_cast<uint8_t*>(ws + P.q8);
   uint8_t* s8 = reinterpret_cast<uint8_t*>(ws + P.s8);
   // encoder Dense layer (query/key/value, attention_output, MLP): bf16/f32 GEMM, or in
@@ -589,6 +615,15 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   rc = patches_launch(images, B, cfg->image_h, cfg->image_w, cfg->channels,
                       cfg->patch_size, patches, kk(d.patch_dim_p), odt, st);
   if (rc) return rc;
+  if (R > d.rows) {                                   // pad rows: zero patches
+    const size_t row_bytes = (size_t)d.patch_dim_p * eop_of(cfg->dtype);
+    VTD_HIP(hipMemsetAsync(static_cast<char*>(patches) + (size_t)d.rows * row_bytes, 0,
+                           (size_t)(R - d.rows) * row_bytes, st));
+    // and the attention output's pad rows, which the attention never writes
+    const size_t attn_row = (size_t)d.inner_p * es_of(cfg->dtype);
+    VTD_HIP(hipMemsetAsync(static_cast<char*>(attn) + (size_t)d.rows * attn_row, 0,
+                           (size_t)(R - d.rows) * attn_row, st));
+  }
   // ---- linear_projection + position embedding add (vtd.py:291-307)
   {
     vtd_epilogue e{};
@@ -732,8 +767,9 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
       if (rc) return rc;
       a = h;
     }
-    rc = gemm_launch(M, VTD_MAX_DETECT, kk(Dp), a, kk(Dp), w->w_det, kk(Dp), gdt, &e, st,
-                     2.0 * fR * D * VTD_MAX_DETECT);
+    // the real rows only (the scatter addresses images by row)
+    rc = gemm_launch((int)d.rows, VTD_MAX_DETECT, kk(Dp), a, kk(Dp), w->w_det, kk(Dp), gdt, &e,
+                     st, 2.0 * fR * D * VTD_MAX_DETECT);
     if (rc) return rc;
   }
   const int HR = (int)d.head_rows;
