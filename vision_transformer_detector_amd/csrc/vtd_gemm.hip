@@ -1929,11 +1929,12 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
 // Fixed targets (not the device's CU count) so that workspace sizing needs no device.
 // VTD_SPLITK=0 / knob VTD_KNOB_SPLITK = 0 disables it.
 constexpr int kSplitTargetDefault = 256, kSplitMinSteps = 8;
-int gemm_splitk_choice(int M, int N, int K, int dtype) {
+int gemm_splitk_choice(int M, int N, int K, int dtype, int target) {
   const int ks = knob(VTD_KNOB_SPLITK);
   if (ks == 0) return 1;
-  // knob value >= 64: the workgroup target itself (A/B of the concurrent micro-batch halves)
-  const int kSplitTarget = ks >= 64 ? ks : kSplitTargetDefault;
+  // knob value >= 64: the workgroup target itself (A/B of the concurrent micro-batch halves);
+  // target > 0: the caller's (vtd_forward: 256 / the concurrent parts)
+  const int kSplitTarget = ks >= 64 ? ks : target > 0 ? target : kSplitTargetDefault;
   if (dtype != VTD_BF16 || N <= 64 || K % 64 != 0 || M <= 0) return 1;
   const int tiles = ((M + BBM - 1) / BBM) * ((N + BBN - 1) / BBN);
   const int nk = K / 64;
@@ -2095,7 +2096,7 @@ extern "C" int vtd_gemm_splitk(int M, int N, int K, const void* A_dev, int lda,
 }
 
 extern "C" int vtd_gemm_splitk_choice(int M, int N, int K, int dtype) {
-  return vtd::gemm_splitk_choice(M, N, K, dtype);
+  return vtd::gemm_splitk_choice(M, N, K, dtype, 0);
 }
 
 #if VTD_DIAG

@@ -26,7 +26,7 @@ int ln_stats_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx, fl
 int ln_stats_finalize_launch(const float* part, int64_t rows, int slots, int D, float eps,
                              float* stat, hipStream_t st);
 bool gemm_emits_stats(int M, int N, int dtype, const vtd_epilogue* e);
-int gemm_splitk_choice(int M, int N, int K, int dtype);
+int gemm_splitk_choice(int M, int N, int K, int dtype, int target = 0);
 int gemm_splitk_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
                        const vtd_epilogue* epi, float* part, int ksplit, hipStream_t stream,
                        double flops);
@@ -244,7 +244,13 @@ bool split_pad() {
   return on;
 }
 // pad: the encoder runs on rows rounded up to whole 256-row GEMM tiles (gemm_rows)
-Plan make_plan(const vtd_config* c, const vtd_dims& d, bool pad = false) {
+// nparts: the micro-batch parts running concurrently (each part's encoder rows are padded
+// when > 1, split_pad; its head's split-K launches target 256 / nparts workgroups, since the
+// parts' head launches co-run: +0.2 % at C2 B = 256, +0.9 % at B = 64,
+// profiles/r05_splitk_target_ab.log)
+int splitk_target(int nparts) { return 256 / std::max(nparts, 1); }
+Plan make_plan(const vtd_config* c, const vtd_dims& d, int nparts = 1) {
+  const bool pad = nparts > 1 && split_pad();
   Plan p{};
   size_t off = 0;
   auto take = [&](size_t bytes) {
@@ -276,7 +282,8 @@ Plan make_plan(const vtd_config* c, const vtd_dims& d, bool pad = false) {
   size_t sk = 0;
   for (int j = 0, k = d.tokens_p; j < d.n_head; k = d.head_units_p[j], ++j) {
     const int s = gemm_splitk_choice((int)HR, d.head_units_p[j], opk(c->dtype, k),
-                                     c->dtype == VTD_BF16X3 ? VTD_BF16 : act_dtype(c->dtype));
+                                     c->dtype == VTD_BF16X3 ? VTD_BF16 : act_dtype(c->dtype),
+                                     splitk_target(nparts));
     if (s > 1) sk = std::max(sk, (size_t)s * HR * d.head_units_p[j] * 4);
   }
   p.splitk = take(sk);
@@ -342,7 +349,7 @@ size_t split_workspace(const vtd_config* c, const vtd_dims& d) {
     const vtd_config sc = sub_config(c, i, ns);
     vtd_dims sd;
     if (derive(&sc, &sd) != VTD_OK) return 0;
-    total += make_plan(&sc, sd, split_pad()).total;
+    total += make_plan(&sc, sd, ns).total;
   }
   return std::max(total, whole);
 }
@@ -386,7 +393,7 @@ SideStream* side_stream(hipStream_t st) {
 // "the GEMM that last wrote x emitted LayerNorm partials" from one stage to the next.
 int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* images,
                  float* logits, float* dets, char* ws, hipStream_t st, int s_lo, int s_hi,
-                 bool& partials, bool pad);
+                 bool& partials, int nparts);
 }  // namespace
 
 }  // namespace vtd
@@ -439,7 +446,7 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
   if (!side) {
     bool partials = false;
     if (ns == 1)
-      return forward_impl(cfg, w, images, logits, dets, ws, st, 0, n_stages, partials, false);
+      return forward_impl(cfg, w, images, logits, dets, ws, st, 0, n_stages, partials, 1);
     // no side stream (first call under capture): the halves run in order on `st`
   }
   const size_t img = (size_t)cfg->image_h * cfg->image_w * cfg->channels;
@@ -486,7 +493,7 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
     P.ws = ws + ws_off;
     P.partials = false;
     b0 += P.cfg.batch;
-    ws_off += make_plan(&P.cfg, dp, split_pad()).total;
+    ws_off += make_plan(&P.cfg, dp, ns).total;
   }
   // Launches are interleaved part by part, one stage (encoder layer) at a time: issuing
   // all of one part's ~110 launches before the next part's first one left the second
@@ -500,7 +507,7 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
       const int s = part == 0 ? t : t - stagger;
       if (s < 0 || s >= n_stages) continue;
       rc = forward_impl(&P.cfg, w, P.images, P.logits, P.dets, P.ws, P.st, s, s + 1, P.partials,
-                        split_pad());
+                        ns);
       if (rc) return rc;
     }
   }
@@ -518,11 +525,12 @@ namespace vtd {
 namespace {
 int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* images,
                  float* logits, float* dets, char* ws, hipStream_t st, int s_lo, int s_hi,
-                 bool& partials, bool pad) {
+                 bool& partials, int nparts) {
   vtd_dims d;
   int rc = derive(cfg, &d);
   if (rc) return rc;
-  const Plan P = make_plan(cfg, d, pad);
+  const Plan P = make_plan(cfg, d, nparts);
+  const bool pad = nparts > 1 && split_pad();
   const bool fp8 = cfg->dtype == VTD_FP8;
   const int dt = act_dtype(cfg->dtype);
   // VTD_BF16X3: every GEMM runs on split-bf16 operands (bf16 kernels over K' = 3 K_p), whose
@@ -780,7 +788,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     e.bias = w->b_head[j]; e.act = act;
     e.out = head[j & 1]; e.ldo = kk(d.head_units_p[j]); e.out_dtype = odt;
     const double fl = 2.0 * HR * (double)kv * d.head_units[j];
-    const int ks = gemm_splitk_choice(HR, d.head_units_p[j], kk(k), gdt);
+    const int ks = gemm_splitk_choice(HR, d.head_units_p[j], kk(k), gdt, splitk_target(nparts));
     rc = ks > 1 ? gemm_splitk_launch(HR, d.head_units_p[j], kk(k), a, kk(k), w->w_head[j], kk(k),
                                      &e, reinterpret_cast<float*>(ws + P.splitk), ks, st, fl)
                 : gemm_launch(HR, d.head_units_p[j], kk(k), a, kk(k), w->w_head[j], kk(k), gdt,
