@@ -1487,18 +1487,24 @@ __global__ __launch_bounds__(BNT) void gemm_mx8_pp_kernel(
       mxp_issue<2>(smem, src, wave, lane, kt + 2, kt & 1);
       mxp_issue<3>(smem, src, wave, lane, kt + 2, kt & 1);
       asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    } else {
+    } else if constexpr (n1) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      // last K-step: every LDS read retired before the barrier, so that G0, released into its
+      // epilogue (LDS staging over the stages) by the next one, cannot overwrite fragments G1
+      // is still reading
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
     pp_barrier();
     mxp_mfma<4, 0>(acc, a, b0, sa, sb);
-    pp_barrier();
+    // the last P3 barrier is G0's alone: G0's epilogue runs beside G1's last MFMA cluster
+    // instead of waiting for it (as pp2_mainloop_2ph; G1 ran one extra barrier first)
+    if (n1 || wm == 0) pp_barrier();
   };
   int kt = 0;
   for (; kt + 2 < nk; ++kt) step(kt, std::true_type{}, std::true_type{});
   if (kt + 1 < nk) step(kt++, std::true_type{}, std::false_type{});
   step(kt, std::false_type{}, std::false_type{});
-  if (wm == 0) pp_barrier();                 // re-align
   float* ep = reinterpret_cast<float*>(smem) + wave * 32 * 68;
   const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
   if constexpr (EPI != EPI_GENERIC) {
