@@ -240,3 +240,48 @@ def _attention_mx8_case(L, cuda, B, N, H, dkp):
     assert torch.equal(q, q_ref)
     v = s.view(inner // 128, s_rows, 4)[:, :rows]
     assert torch.equal(v, s_ref.view(inner // 128, s_rows, 4)[:, :rows])
+
+
+@pytest.mark.parametrize("M,N,K,act,out_dtype,resid", [
+    (4096, 1024, 1024, 1, 2, False), (1536, 2048, 768, 2, 2, False), (2304, 1280, 640, 2, 1, False),
+    (4096, 768, 1536, 1, 1, True), (1000, 520, 384, 1, 0, False)])
+def test_gemm_mx8_transposed_equals_staged(L, cuda, M, N, K, act, out_dtype, resid):
+    """Activation layers without a residual take the transposed-accumulator MX kernel
+    (operands swapped in the scaled MFMA, permuted B rows with their scales, register-direct
+    epilogue incl. the MX-fp8 output); knob VTD_KNOB_GEMM_TR = 0 keeps the staged epilogue
+    (the residual case checks the knob is harmless where no transposed kernel exists).  The same products in the
+    same order: the outputs (and the MX-fp8 scales) are identical."""
+    g = torch.Generator(device=cuda).manual_seed(M + N + K + 11)
+    A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
+    W = torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)
+    qa, sa, sa_rows = _quantize(L, A, K)
+    qb, sb, sb_rows = _quantize(L, W, K)
+    bias = torch.randn(N, generator=g, device=cuda)
+    res0 = torch.randn(M, N, generator=g, device=cuda).to(
+        torch.float32 if out_dtype == 0 else torch.bfloat16)
+
+    def run():
+        if out_dtype == 2:
+            out = torch.full((M, N), 0x7f, dtype=torch.uint8, device=cuda)
+            s = torch.full((N // 128 * sa_rows * 4,), 0xff, dtype=torch.uint8, device=cuda)
+        else:
+            out = res0.clone() if resid else torch.zeros_like(res0)
+            s = None
+        e = L.VtdEpilogue()
+        e.bias, e.act, e.out, e.ldo, e.out_dtype = bias.data_ptr(), act, out.data_ptr(), N, out_dtype
+        if resid:
+            e.resid, e.ldr = out.data_ptr(), N
+        if s is not None:
+            e.scale_out, e.scale_rows = s.data_ptr(), sa_rows
+        L.check(L.lib.vtd_gemm_mx8(M, N, K, qa.data_ptr(), K, sa.data_ptr(), sa_rows,
+                                   qb.data_ptr(), K, sb.data_ptr(), sb_rows, ctypes.byref(e),
+                                   L.stream_ptr()), "gemm_mx8")
+        torch.cuda.synchronize()
+        return out, s
+
+    got, gs = run()
+    with L.knob(L.KNOB_GEMM_TR, 0):
+        ref_out, rs = run()
+    assert torch.equal(got, ref_out)
+    if gs is not None:
+        assert torch.equal(gs, rs)

@@ -872,6 +872,8 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
   constexpr bool OUT_BF16 = (EPI & 4) != 0;
   constexpr bool RESID = (EPI & 8) != 0 && !(DG & 2);
   constexpr bool LNF = (EPI & EPI_LNF) != 0, STAT = (EPI & EPI_STAT) != 0 && !(DG & 1);
+  constexpr bool F8O = (EPI & EPI_F8O) != 0;
+  static_assert(!(F8O && (STAT || (EPI & EPI_S3) != 0)), "MX-fp8 output: no statistics / split");
   const int fr = lane & 15, fg = lane >> 4;
   f32x4 bias[2][2], cs[2][2] = {};
 #pragma unroll
@@ -950,6 +952,30 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
         }
         if constexpr ((EPI & EPI_O2) != 0) epi_out2_8(e, mrow, ncol, v0, v1);
         const int64_t idx = (int64_t)mrow * e.ldo + ncol;
+        if constexpr (F8O) {
+          // the next MX GEMM's operand: the 32-column block 32 jp .. + 31 of row mrow is the
+          // lanes fr, fr + 16, fr + 32, fr + 48 (fg = 0..3): block amax by the two lane swaps;
+          // bf16-rounded values, so the bytes equal vtd_quantize_mx8 of the bf16 output
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v0[j] = bf16_round(v0[j]);
+            v1[j] = bf16_round(v1[j]);
+          }
+          float am = 0.f;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) am = fmaxf(am, fmaxf(fabsf(v0[j]), fabsf(v1[j])));
+          am = xmax32(xmax16(am));
+          const int E = mx8_exponent(am);
+          const float inv = __uint_as_float((uint32_t)(127 - E) << 23);
+          const uint2 qv = {mx8_pack4(v0[0], v0[1], v0[2], v0[3], inv),
+                            mx8_pack4(v1[0], v1[1], v1[2], v1[3], inv)};
+          *reinterpret_cast<uint2*>(static_cast<uint8_t*>(e.out) + idx) = qv;
+          if (fg == 0) {
+            const int b = (n_base + 32 * jp) >> 5;
+            e.sout[((int64_t)(b >> 2) * e.s_rows + mrow) * 4 + (b & 3)] = (uint8_t)(E + 127);
+          }
+          continue;
+        }
         if constexpr (OUT_BF16) {
           const i32x4 o = {(int)pack_bf16x2(v0[0], v0[1]), (int)pack_bf16x2(v0[2], v0[3]),
                            (int)pack_bf16x2(v1[0], v1[1]), (int)pack_bf16x2(v1[2], v1[3])};
@@ -1359,7 +1385,10 @@ __device__ __forceinline__ i32x8_t mx_operand(const bf16x8& lo, const bf16x8& hi
                                  1, 2, 3, 4, 5, 6, 7);
 }
 
-template <int I0, int J0>
+// TR: the transposed-accumulator variant (operands swapped, B rows permuted, as pp_mfma_t):
+// a lane's accumulators are 8 contiguous output columns of one row, for the register-direct
+// epilogue; sb then holds the scales of the permuted B rows the lane supplies
+template <int I0, int J0, bool TR = false>
 __device__ __forceinline__ void mxp_mfma(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][2],
                                          const bf16x8 (&b)[2][2], const int (&sa)[8],
                                          const int (&sb)[4]) {
@@ -1368,9 +1397,14 @@ __device__ __forceinline__ void mxp_mfma(f32x4 (&acc)[8][4], const bf16x8 (&a)[4
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      acc[I0 + i][J0 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-          mx_operand(a[i][0], a[i][1]), mx_operand(b[j][0], b[j][1]), acc[I0 + i][J0 + j], 0, 0,
-          0, sa[I0 + i], 0, sb[J0 + j]);
+      if constexpr (TR)
+        acc[I0 + i][J0 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+            mx_operand(b[j][0], b[j][1]), mx_operand(a[i][0], a[i][1]), acc[I0 + i][J0 + j], 0,
+            0, 0, sb[J0 + j], 0, sa[I0 + i]);
+      else
+        acc[I0 + i][J0 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+            mx_operand(a[i][0], a[i][1]), mx_operand(b[j][0], b[j][1]), acc[I0 + i][J0 + j], 0,
+            0, 0, sa[I0 + i], 0, sb[J0 + j]);
   // pin the cluster inside its phase: without these the compiler sinks every scaled MFMA
   // of the K-step past the phase barriers to the end of the loop body (no ping-pong left)
 #pragma unroll
@@ -1380,7 +1414,7 @@ __device__ __forceinline__ void mxp_mfma(f32x4 (&acc)[8][4], const bf16x8 (&a)[4
   __builtin_amdgcn_s_setprio(0);
 }
 
-template <int EPI>
+template <int EPI, bool TR = false>
 __global__ __launch_bounds__(BNT) void gemm_mx8_pp_kernel(
     int M, int N, int K, const uint8_t* __restrict__ A, int lda, const uint8_t* __restrict__ sA,
     int64_t sa_rows, const uint8_t* __restrict__ Bt, int ldb, const uint8_t* __restrict__ sB,
@@ -1409,13 +1443,15 @@ __global__ __launch_bounds__(BNT) void gemm_mx8_pp_kernel(
     src.rsb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(sB), 0,
                                                 (int)std::min<int64_t>(sb_rows * K / 32, 0x7fffffff), 0x00020000);
     const int prow = lane >> 3, pchunk = (lane & 7) ^ prow;
+    // transposed variant: B groups in the swz_t image (as pp2b_sources)
+    const int bchunk = TR ? pchunk ^ ((wave & 1) << 2) : pchunk;
 #pragma unroll
     for (int g = 0; g < 4; ++g)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int tr = grp_tile_row(g, (wave * 2 + j) * 8 + prow);
         src.off[g][j] = g < 2 ? min(tr, M - 1 - m0) * lda + pchunk * 16
-                              : min(tr, N - 1 - n0) * ldb + pchunk * 16;
+                              : min(tr, N - 1 - n0) * ldb + bchunk * 16;
       }
     // scales: lanes 0-7 of wave w copy the dwords of tile rows 32 w + 4 l .. + 3 (rows past
     // the end read beyond sa_rows / sb_rows fall outside the records: zero)
@@ -1456,31 +1492,36 @@ __global__ __launch_bounds__(BNT) void gemm_mx8_pp_kernel(
     constexpr bool n1 = decltype(t1)::value, n2 = decltype(t2)::value;
     // ---- P0 (also every scale of the tile: X0 / Y0 refill them two tiles ahead)
     pp_load_a(a, st + 0 * 16384, ra, fr, fg);
-    pp_load_b(b0, st + 2 * 16384, rb, fr, fg);
+    if constexpr (TR) pp_load_b_t(b0, st + 2 * 16384, rb, fr, fg);
+    else pp_load_b(b0, st + 2 * 16384, rb, fr, fg);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
       sa[i] = *reinterpret_cast<const int*>(st + BSTAGE + (sa_row + 16 * i) * 4) >> (8 * fg);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      sb[j] = *reinterpret_cast<const int*>(st + BSTAGE + 1024 + (sb_row + 16 * j) * 4) >> (8 * fg);
+    for (int j = 0; j < 4; ++j)     // TR: block j of a 32-row half holds rows perm_t(j & 1, fr)
+      sb[j] = *reinterpret_cast<const int*>(
+                  st + BSTAGE + 1024 +
+                  (TR ? wn * 64 + 32 * (j >> 1) + perm_t(j & 1, fr) : sb_row + 16 * j) * 4) >>
+              (8 * fg);
     if constexpr (n1) mxp_issue<1>(smem, src, wave, lane, kt + 1, (kt + 1) & 1);
     if constexpr (n1) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     pp_barrier();
-    mxp_mfma<0, 0>(acc, a, b0, sa, sb);
+    mxp_mfma<0, 0, TR>(acc, a, b0, sa, sb);
     pp_barrier();
     // ---- P1
-    pp_load_b(b1, st + 3 * 16384, rb, fr, fg);
+    if constexpr (TR) pp_load_b_t(b1, st + 3 * 16384, rb, fr, fg);
+    else pp_load_b(b1, st + 3 * 16384, rb, fr, fg);
     if constexpr (n1) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     pp_barrier();
-    mxp_mfma<0, 2>(acc, a, b1, sa, sb);
+    mxp_mfma<0, 2, TR>(acc, a, b1, sa, sb);
     pp_barrier();
     // ---- P2
     pp_load_a(a, st + 1 * 16384, ra, fr, fg);
     if constexpr (n2) mxp_issue<0>(smem, src, wave, lane, kt + 2, kt & 1);
     pp_barrier();
-    mxp_mfma<4, 2>(acc, a, b1, sa, sb);
+    mxp_mfma<4, 2, TR>(acc, a, b1, sa, sb);
     pp_barrier();
     // ---- P3
     if constexpr (n2) {
@@ -1496,7 +1537,7 @@ __global__ __launch_bounds__(BNT) void gemm_mx8_pp_kernel(
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
     pp_barrier();
-    mxp_mfma<4, 0>(acc, a, b0, sa, sb);
+    mxp_mfma<4, 0, TR>(acc, a, b0, sa, sb);
     // the last P3 barrier is G0's alone: G0's epilogue runs beside G1's last MFMA cluster
     // instead of waiting for it (as pp2_mainloop_2ph; G1 ran one extra barrier first)
     if (n1 || wm == 0) pp_barrier();
@@ -1507,6 +1548,16 @@ __global__ __launch_bounds__(BNT) void gemm_mx8_pp_kernel(
   step(kt, std::false_type{}, std::false_type{});
   float* ep = reinterpret_cast<float*>(smem) + wave * 32 * 68;
   const int m_base = m0 + wm * 128, n_base = n0 + wn * 64;
+  if constexpr (TR) {
+    if constexpr (EPI != EPI_GENERIC) {
+      if (m0 + BBM <= M && n0 + BBN <= N) {
+        epilogue_direct<EPI>(acc, lane, m_base, n_base, e);
+        return;
+      }
+    }
+    epilogue_direct_generic(acc, ep, lane, M, N, m_base, n_base, e);
+    return;
+  }
   if constexpr (EPI != EPI_GENERIC) {
     if (m0 + BBM <= M && n0 + BBN <= N) {
       epilogue_fast<EPI>(acc, ep, lane, m_base, n_base, e);
@@ -1998,6 +2049,12 @@ int gemm_splitk_launch(int M, int N, int K, const void* A, int lda, const void* 
   return VTD_OK;
 }
 
+// the MX-fp8 epilogue codes with a transposed-accumulator kernel: the activation layers
+// without a residual (bias + act, f32 / bf16 / MX-fp8 out) and the generic path of partial
+// tiles.  C5 per launch (profiles/r05_mx_transposed_ab.log): mlp1 (MX-fp8 out) -5 %, mlp2
+// -3 %; the residual layer mlp3 +3 % (not transposed)
+#define VTD_MX_TR_CODES(X) X(EPI_GENERIC) X(0) X(1) X(2) X(4) X(5) X(6) X(5 | EPI_F8O) \
+  X(6 | EPI_F8O)
 int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_t* sA,
                     int64_t sa_rows, const uint8_t* Bt, int ldb, const uint8_t* sB,
                     int64_t sb_rows, const vtd_epilogue* epi, hipStream_t stream,
@@ -2040,11 +2097,14 @@ int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_
   static std::once_flag once[kMaxDevices];
   once_per_device(once, [] {
 #define VTD_MX_FN(C) reinterpret_cast<const void*>(&gemm_mx8_pp_kernel<C>),
+#define VTD_MXT_FN(C) reinterpret_cast<const void*>(&gemm_mx8_pp_kernel<C, true>),
     const void* fns[] = {VTD_MX_FN(EPI_GENERIC) VTD_MX_FN(0) VTD_MX_FN(1) VTD_MX_FN(2)
                          VTD_MX_FN(4) VTD_MX_FN(5) VTD_MX_FN(6) VTD_MX_FN(8) VTD_MX_FN(9)
                          VTD_MX_FN(10) VTD_MX_FN(12) VTD_MX_FN(13) VTD_MX_FN(14)
-                         VTD_MX_FN(4 | EPI_F8O) VTD_MX_FN(5 | EPI_F8O) VTD_MX_FN(6 | EPI_F8O)};
+                         VTD_MX_FN(4 | EPI_F8O) VTD_MX_FN(5 | EPI_F8O) VTD_MX_FN(6 | EPI_F8O)
+                         VTD_MX_TR_CODES(VTD_MXT_FN)};
 #undef VTD_MX_FN
+#undef VTD_MXT_FN
     for (const void* f : fns)
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * MXP_STAGE);
   });
@@ -2057,6 +2117,24 @@ int gemm_mx8_launch(int M, int N, int K, const uint8_t* A, int lda, const uint8_
                               (e.out_dtype == VTD_FP8 ? EPI_F8O : 0)
                         : EPI_GENERIC;
   const dim3 g(tiles_m * tiles_n), b(BNT);
+  // transposed accumulators + register-direct epilogue for the activation layers (as the bf16
+  // kernels; knob VTD_KNOB_GEMM_TR = 0 keeps the staged epilogue everywhere)
+  // (1: every layer without a residual, also query/key/value and the plain ones)
+  const int ktr = knob(VTD_KNOB_GEMM_TR);
+  const bool tr = !e.resid && (ktr == 1 || (ktr != 0 && e.act != VTD_ACT_NONE));
+  if (tr) {
+    switch (code) {
+#define VTD_MXT_CASE(C)                                                                         \
+  case C:                                                                                       \
+    hipLaunchKernelGGL((gemm_mx8_pp_kernel<C, true>), g, b, 2 * MXP_STAGE, stream, M, N, K, A,  \
+                       lda, sA, sa_rows, Bt, ldb, sB, sb_rows, tiles_m, tiles_n, e);            \
+    VTD_LAUNCH_CHECK("gemm_mx8");                                                               \
+    return VTD_OK;
+      VTD_MX_TR_CODES(VTD_MXT_CASE)
+#undef VTD_MXT_CASE
+      default: break;
+    }
+  }
   switch (code) {
 #define VTD_MX_CASE(C)                                                                       \
   case C:                                                                                    \
