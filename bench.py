@@ -590,7 +590,13 @@ def main():
                          kw, model.dims, B, 4 if (args.dtype in ("f32", "float32") or
                                               os.environ.get("VTD_RESID_F32", "0") != "0") else 2)),
                      "avg_launch_us": round(g["avg_us"], 2),
-                     "launches_per_step": g["launches"] // max(1, args.steps)},
+                     "launches_per_step": g["launches"] // max(1, args.steps),
+                     # the GEMM class in the TIMED step (two streams: tails filled, epilogues
+                     # beside the other part's K loops): its algorithmic FLOPs per step over
+                     # the whole step time (non-GEMM kernels included) -- a lower bound of the
+                     # GEMMs' in-step rate; frac above is the isolated-launch figure
+                     "step_frac": round(fl[0] / max(1, args.steps) / (ms_per_step * 1e-3) /
+                                        (peak * 1e12), 4) if fl[0] > 0 else None},
         "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv)
                         for kk, vv in v.items()} for k, v in kernels.items()},
         "profiled_ms_per_step": round(1e3 * prof_elapsed / args.steps, 3),
