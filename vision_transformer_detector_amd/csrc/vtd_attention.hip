@@ -1232,7 +1232,7 @@ int launch_bf16_ps16(const void* qkv, int B, int N, int heads, int ldqkv, float 
 #endif  // VTD_DIAG
 
 int launch_bf16_ps(const void* qkv, int B, int N, int heads, int ldqkv, float scale, void* out,
-                   int ldo, hipStream_t stream) {
+                   int ldo, hipStream_t stream, int parts) {
   const int NR = (N + 31) & ~31;
   const int lds = 5 * NR * 128;
   static std::once_flag once[kMaxDevices];
@@ -1246,10 +1246,11 @@ int launch_bf16_ps(const void* qkv, int B, int N, int heads, int ldqkv, float sc
   });
   const int ncu = device_cu_count();
   const int npairs = B * heads;
-  // workgroups: one per CU (knob VTD_KNOB_ATTN_GRID overrides: A/B of co-running the two
-  // micro-batch streams' attention on disjoint halves of the chip)
+  // workgroups: one per CU, divided by the concurrent micro-batch parts of a split forward
+  // (their attention launches co-run: half the chip each, +0.2 % at C2 B = 256, +0.4 % at
+  // B = 64, profiles/r05_attn_grid_ab.log); knob VTD_KNOB_ATTN_GRID overrides
   const int kg = knob(VTD_KNOB_ATTN_GRID);
-  const int grid = std::min(npairs, kg > 0 ? kg : ncu);
+  const int grid = std::min(npairs, kg > 0 ? kg : ncu / std::max(parts, 1));
   // the last block's 8-key groups holding keys < N (1, 2 or 4 = untrimmed)
   const int tail = N - (NR - 32), tg = tail <= 8 ? 1 : tail <= 16 ? 2 : 4;
 #define VTD_PS_PICK(NB) (tg == 1 ? attention_bf16_ps_kernel<NB, 1>                          \
@@ -1352,7 +1353,7 @@ int launch(const void* qkv, int B, int N, int heads, int ldqkv, float scale, voi
 
 int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqkv,
                      float scale, void* out, int ldo, int dtype, hipStream_t stream,
-                     double flops) {
+                     double flops, int parts) {
   VTD_CHECK_ARG(qkv && out, "attention: null pointer");
   VTD_CHECK_ARG(B > 0 && N > 0 && heads > 0, "attention: bad B/N/heads");
   VTD_CHECK_ARG(dkp == 32 || dkp == 64 || dkp == 128, "attention: dkp must be 32/64/128");
@@ -1377,7 +1378,7 @@ int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqk
       return launch_bf16_ps16(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
 #endif
     if ((v1 == 4 || v1 == 5) && ps_ok)
-      return launch_bf16_ps(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+      return launch_bf16_ps(qkv, B, N, heads, ldqkv, scale, out, ldo, stream, parts);
     // 6: the long-sequence LDS-DMA kernel (dkp 64, any N; opt-in: measured slower than the
     // streaming kernel at C3 / C5, profiles/r05_attn_fl_ab.log)
     if (dkp == 64 && ldqkv % 8 == 0 && ldo % 8 == 0 && v1 == 6)
@@ -1434,5 +1435,5 @@ extern "C" int vtd_attention(const void* qkv_dev, int B, int N, int heads, int d
                              int ldqkv, float scale, void* out_dev, int ldo, int dtype,
                              void* stream) {
   return vtd::attention_launch(qkv_dev, B, N, heads, dkp, ldqkv, scale, out_dev, ldo,
-                               dtype, static_cast<hipStream_t>(stream), 0.0);
+                               dtype, static_cast<hipStream_t>(stream), 0.0, 1);
 }

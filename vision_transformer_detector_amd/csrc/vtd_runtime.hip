@@ -18,7 +18,7 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
                    const float* lnpart, int lnslots, int lnD, float lneps);
 int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqkv,
                      float scale, void* out, int ldo, int dtype, hipStream_t stream,
-                     double flops);
+                     double flops, int parts = 1);
 int layernorm_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx, const float* g,
                      const float* b, float eps, void* y, int ldy, int dtype, hipStream_t st);
 int ln_stats_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx, float eps,
@@ -684,7 +684,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
          : attn_mx8 ? attention_mx8_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale,
                                          q8, d.inner_p, s8, P.s8_rows, st, attn_flops)
                   : attention_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale,
-                                     attn, d.inner_p, dt, st, attn_flops);
+                                     attn, d.inner_p, dt, st, attn_flops, nparts);
     if (rc) return rc;
     // VTD_BF16X3: the f32 attention output split into the attention_output GEMM's operand
     const void* attn_op = attn;
