@@ -221,12 +221,14 @@ def test_two_stream_split_stagger_is_bit_exact(vtd, cuda, stagger):
     assert torch.equal(got, ref)
 
 
-def test_two_stream_split_graph_capture(vtd, cuda):
+@pytest.mark.parametrize("batch", [128, 130])
+def test_two_stream_split_graph_capture(vtd, cuda, batch):
     """The split forward (fork / join events to the internal stream) is HIP-graph
-    capturable: the replay reproduces the eager result exactly."""
+    capturable: the replay reproduces the eager result exactly (130 images: parts padded
+    to whole 256-row tiles, the pad rows zeroed by memsets inside the capture)."""
     model = vtd.create_vision_transformer_detector(**SPLIT_KW, dtype="bfloat16", seed=4)
     g = torch.Generator(device=cuda).manual_seed(2)
-    x = torch.rand(128, 224, 224, 3, generator=g, device=cuda) * 2 - 1
+    x = torch.rand(batch, 224, 224, 3, generator=g, device=cuda) * 2 - 1
     eager = model(x).clone()
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
