@@ -181,7 +181,7 @@ SPLIT_KW = dict(input_shape=(224, 224, 3), patch_size=16, embedding_dim=64, enco
                 mlp_head_last_units=8, mlp_head_dense_layers_quantity=2)
 
 
-@pytest.mark.parametrize("batch", [128, 130])
+@pytest.mark.parametrize("batch", [128, 129, 130])
 @pytest.mark.parametrize("dtype", ["float32", "bf16x3", "bfloat16"])
 def test_two_stream_split_matches_single_images(vtd, cuda, dtype, batch):
     """A batch large enough for vtd_forward's two-stream micro-batching (128 x 196 rows:
@@ -189,7 +189,8 @@ def test_two_stream_split_matches_single_images(vtd, cuda, dtype, batch):
     the result it gets alone: bit-exact in float32 (one GEMM kernel for every M), within
     the bf16 tolerance against a single-image forward in bfloat16 (the 256-tile kernels
     only serve the large batch).  130 images: halves of 65 x 196 = 12740 rows, which the
-    parts pad to 12800 (whole 256-row tiles; the pad rows must not reach any image)."""
+    parts pad to 12800 (whole 256-row tiles; the pad rows must not reach any image); 129:
+    unequal parts (64 + 65 images, 12544 rows unpadded + 12740 padded)."""
     model = vtd.create_vision_transformer_detector(**SPLIT_KW, dtype=dtype, seed=3)
     g = torch.Generator(device=cuda).manual_seed(1)
     x = torch.rand(batch, 224, 224, 3, generator=g, device=cuda) * 2 - 1
