@@ -542,10 +542,21 @@ __device__ __forceinline__ int swz_v(int row) { return ((row >> 1) & 1) << 2; }
 template <int NB, int TG = 4>   // key blocks of 32: N in (32 (NB - 1), 32 NB]
 __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
     const bf16_t* __restrict__ qkv, int npairs, int N, int heads, int ldqkv, float scale_log2,
-    bf16_t* __restrict__ out, int ldo) {
+    bf16_t* __restrict__ out, int ldo, int dmode_arg) {
   constexpr int DKP = 64;
   typedef __attribute__((address_space(3))) void lds_void_t;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // diagnostic build only (timing experiments, wrong results; knob VTD_ATTN_DMODE): bit 0
+  // reads each image's Q / K / V as head-major [part][head][N][64] blocks, bit 1 skips the
+  // compute (DMAs + stores only), bit 2 skips the DMAs (compute on stale LDS), bit 3 replaces
+  // the exponential by a multiply, bit 4 skips the V DMAs, bit 5 the K reads of the scores
+  // (Q fragments as both operands), bit 6 the V reads of the PV steps (P as both operands)
+#if VTD_DIAG
+  const int dmode = dmode_arg;
+#else
+  constexpr int dmode = 0;
+  (void)dmode_arg;
+#endif
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, half = lane >> 5, col = lane & 31;
   const int NR = (N + 31) & ~31;
@@ -553,7 +564,7 @@ __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
   char* const qarea = smem + 2 * SLOT;
   const int inner = heads * DKP;
   const int q0 = wave * 32;
-  const bool active = q0 < N;
+  const bool active = q0 < N && !(dmode & 2);
   const int G = gridDim.x;
   const int ngroups = NR >> 3;                   // 8-row groups per matrix
   const int lrow = lane >> 3, lchunk = lane & 7;
@@ -566,10 +577,13 @@ __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<bf16_t*>(qkv + (int64_t)b * N * ldqkv), 0, N * ldqkv * 2, 0x00020000);
     const int colb = (part * inner + h * DKP) * 2;
-    for (int g = wave; g < ngroups; g += 8) {
+    const bool skip = (dmode & 4) || ((dmode & 16) && part == 2);
+    for (int g = skip ? ngroups : wave; g < ngroups; g += 8) {
       const int r = g * 8 + lrow;
       const int sw = part == 2 ? swz_v(r) : swz_kq(r);
-      const int voff = min(r, N - 1) * ldqkv * 2 + colb + ((lchunk ^ sw) << 4);
+      const int voff = (dmode & 1)
+                           ? ((part * heads + h) * N + min(r, N - 1)) * 128 + ((lchunk ^ sw) << 4)
+                           : min(r, N - 1) * ldqkv * 2 + colb + ((lchunk ^ sw) << 4);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + g * 1024), 16, voff, 0, 0,
                                                0);
     }
@@ -626,8 +640,9 @@ __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
 #pragma unroll
         for (int st = 0; st < 4; ++st)
           s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              *reinterpret_cast<const bf16x8*>(krow + (((st * 2 + half) ^ swk) << 4)), qf[st],
-              s[kb], 0, 0, 0);
+              (dmode & 32) ? qf[st]
+                           : *reinterpret_cast<const bf16x8*>(krow + (((st * 2 + half) ^ swk) << 4)),
+              qf[st], s[kb], 0, 0, 0);
       }
       if (N < NB * 32) {                        // keys >= N of the last block
 #pragma unroll
@@ -659,6 +674,7 @@ __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
       // 16-key PV steps of block kb: 1 for a trimmed last block (TG <= 2)
       auto nsteps = [](int kb) { return (kb == NB - 1 && TG <= 2) ? 1 : 2; };
       auto vread = [&](int kb, bf16x4 (&f)[2][2][2]) {
+        if (dmode & 64) return;
 #pragma unroll
         for (int st = 0; st < nsteps(kb); ++st)
 #pragma unroll
@@ -683,7 +699,8 @@ __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
               e[j] = 0.f;
               continue;
             }
-            e[j] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][8 * st + j], scale_log2, nmx));
+            e[j] = (dmode & 8) ? __builtin_fmaf(s[kb][8 * st + j], scale_log2, nmx)
+                               : __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][8 * st + j], scale_log2, nmx));
             if (j & 1) ps1 += e[j];
             else ps0 += e[j];
           }
@@ -707,7 +724,8 @@ __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
           for (int db = 0; db < 2; ++db) {
             const bf16x4 lo = vf[kb & 1][st][db][0], hi = vf[kb & 1][st][db][1];
             const bf16x8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb[st], o[db], 0, 0, 0);
+            o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16((dmode & 64) ? pb[st] : a, pb[st],
+                                                            o[db], 0, 0, 0);
           }
       }
       l_run = ps0 + ps1;
@@ -1260,9 +1278,14 @@ int launch_bf16_ps(const void* qkv, int B, int N, int heads, int ldqkv, float sc
                : NR == 224 ? VTD_PS_PICK(7)
                            : VTD_PS_PICK(8);
 #undef VTD_PS_PICK
+#if VTD_DIAG
+  static const int dmode = getenv("VTD_ATTN_DMODE") ? atoi(getenv("VTD_ATTN_DMODE")) : 0;
+#else
+  constexpr int dmode = 0;
+#endif
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, stream, static_cast<const bf16_t*>(qkv),
                      npairs, N, heads, ldqkv, scale * 1.4426950408889634f,
-                     static_cast<bf16_t*>(out), ldo);
+                     static_cast<bf16_t*>(out), ldo, dmode);
   VTD_LAUNCH_CHECK("attention_bf16_ps");
   return VTD_OK;
 }

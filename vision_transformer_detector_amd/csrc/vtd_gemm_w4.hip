@@ -294,17 +294,7 @@ __device__ __forceinline__ f32x4 w4_acc(const f32x4& a) {
 constexpr int W4_LNFOLD = 16;
 // EPI bit 32 (the MX-fp8 x4 kernel only): MX-fp8 output (out_dtype VTD_FP8, e.sout scales)
 constexpr int W4_FP8OUT = 32;
-// max of v over lanes l, l ^ 16 (xmax16) / l, l ^ 32 (xmax32)
-__device__ __forceinline__ float xmax16(float v) {
-  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false,
-                                                  false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
-__device__ __forceinline__ float xmax32(float v) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false,
-                                                  false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
+// xmax16 / xmax32: vtd_gemm_epi.h
 template <int EPI>
 struct W4Cols {
   static constexpr int NC = (EPI & W4_LNFOLD) ? 4 : 1;
