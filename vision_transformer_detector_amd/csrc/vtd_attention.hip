@@ -550,7 +550,8 @@ __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
   // reads each image's Q / K / V as head-major [part][head][N][64] blocks, bit 1 skips the
   // compute (DMAs + stores only), bit 2 skips the DMAs (compute on stale LDS), bit 3 replaces
   // the exponential by a multiply, bit 4 skips the V DMAs, bit 5 the K reads of the scores
-  // (Q fragments as both operands), bit 6 the V reads of the PV steps (P as both operands)
+  // (Q fragments as both operands), bit 6 the V reads of the PV steps (P as both operands),
+  // bit 7 an XCD-major pair order (below)
 #if VTD_DIAG
   const int dmode = dmode_arg;
 #else
@@ -589,7 +590,9 @@ __global__ __launch_bounds__(512, 1) void attention_bf16_ps_kernel(
     }
   };
 
-  int p = blockIdx.x;
+  // bit 7: the workgroups of one XCD (blockIdx % 8) take consecutive pairs (all heads of an
+  // image on one XCD's L2) -- needs a grid that is a multiple of 8
+  int p = (dmode & 128) ? (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3) : blockIdx.x;
   if (p >= npairs) return;                       // uniform per workgroup
   issue(p, 1, smem);
   issue(p, 2, smem + NR * 128);
