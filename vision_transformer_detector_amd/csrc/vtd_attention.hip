@@ -401,24 +401,25 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
 #pragma unroll
           for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
       }
-      // score pairs through the packed fp32 VALU (v_pk_fma_f32 / v_pk_add_f32: two lanes'
-      // worth per instruction), the exponentials one by one (no packed v_exp_f32)
-      f32x2 psum = {0.f, 0.f};
-      const f32x2 sc2 = {scale_log2, scale_log2}, nm2 = {-m_run, -m_run};
+      // scalar fp32 VALU (v_fma_f32 / v_add_f32; the file is built without SLP packing):
+      // packed f32 ops cost more issue cycles beside MFMAs than two scalar ones; even / odd
+      // scores summed apart
+      float ps0 = 0.f, ps1 = 0.f;
+      const float nm = -m_run;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
         if (kb < nkb) {
 #pragma unroll
           for (int r = 0; r < 16; r += 2) {
-            f32x2 p = __builtin_elementwise_fma(f32x2{s[kb][r], s[kb][r + 1]}, sc2, nm2);
-            p.x = __builtin_amdgcn_exp2f(p.x);
-            p.y = __builtin_amdgcn_exp2f(p.y);
-            s[kb][r] = p.x;
-            s[kb][r + 1] = p.y;
-            psum += p;
+            const float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][r], scale_log2, nm));
+            const float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][r + 1], scale_log2, nm));
+            s[kb][r] = p0;
+            s[kb][r + 1] = p1;
+            ps0 += p0;
+            ps1 += p1;
           }
         }
-      l_run += psum.x + psum.y;
+      l_run += ps0 + ps1;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
         if (kb < nkb) {
