@@ -1483,7 +1483,12 @@ __global__ __launch_bounds__(BNT) void gemm_mx8_pp_kernel(
   pp_barrier();
   if (wm == 1) pp_barrier();                 // stagger G1 by one barrier
   const int ra = wm * 64, rb = wn * 32;      // group rows of this wave's quads
-  const int sa_row = wm * 128 + fr, sb_row = wn * 64 + fr;
+  // scale bytes: a lane's K-block is fg, i.e. byte fg of each row's scale dword, read as a
+  // byte (the instruction takes byte 0 of the scale register: no shift); the lane-constant
+  // offsets are hoisted, the row-block steps are immediates (TR: perm_t(1, fr) =
+  // perm_t(0, fr) + 4)
+  const int sa_lane = BSTAGE + (wm * 128 + fr) * 4 + fg;
+  const int sb_lane = BSTAGE + 1024 + (TR ? wn * 64 + perm_t(0, fr) : wn * 64 + fr) * 4 + fg;
   bf16x8 a[4][2], b0[2][2], b1[2][2];
   int sa[8], sb[4];
   // one K-step, the last two peeled at compile time (as pp2_mainloop)
@@ -1494,15 +1499,13 @@ __global__ __launch_bounds__(BNT) void gemm_mx8_pp_kernel(
     pp_load_a(a, st + 0 * 16384, ra, fr, fg);
     if constexpr (TR) pp_load_b_t(b0, st + 2 * 16384, rb, fr, fg);
     else pp_load_b(b0, st + 2 * 16384, rb, fr, fg);
+    const uint8_t* ssa = reinterpret_cast<const uint8_t*>(st) + sa_lane;
+    const uint8_t* ssb = reinterpret_cast<const uint8_t*>(st) + sb_lane;
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-      sa[i] = *reinterpret_cast<const int*>(st + BSTAGE + (sa_row + 16 * i) * 4) >> (8 * fg);
+    for (int i = 0; i < 8; ++i) sa[i] = ssa[64 * i];
 #pragma unroll
     for (int j = 0; j < 4; ++j)     // TR: block j of a 32-row half holds rows perm_t(j & 1, fr)
-      sb[j] = *reinterpret_cast<const int*>(
-                  st + BSTAGE + 1024 +
-                  (TR ? wn * 64 + 32 * (j >> 1) + perm_t(j & 1, fr) : sb_row + 16 * j) * 4) >>
-              (8 * fg);
+      sb[j] = ssb[TR ? 4 * (32 * (j >> 1) + 4 * (j & 1)) : 64 * j];
     if constexpr (n1) mxp_issue<1>(smem, src, wave, lane, kt + 1, (kt + 1) & 1);
     if constexpr (n1) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
