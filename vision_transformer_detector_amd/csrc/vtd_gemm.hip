@@ -420,11 +420,8 @@ __device__ __forceinline__ void epilogue_fast(const f32x4 (&acc)[8][4], float* e
           // the next MX GEMM's operand: a 32-column block = 4 consecutive lanes (c8 / 8
           // = 0..3 or 4..7), block amax by DPP quad xor 1 / xor 2; bf16-rounded values so
           // the bytes equal vtd_quantize_mx8 of the bf16 output
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            v0[j] = bf16_round(v0[j]);
-            v1[j] = bf16_round(v1[j]);
-          }
+          bf16_round4(v0);
+          bf16_round4(v1);
           float am = 0.f;
 #pragma unroll
           for (int j = 0; j < 4; ++j) am = fmaxf(am, fmaxf(fabsf(v0[j]), fabsf(v1[j])));
@@ -956,11 +953,8 @@ __device__ __forceinline__ void epilogue_direct(const f32x4 (&acc)[8][4], int la
           // the next MX GEMM's operand: the 32-column block 32 jp .. + 31 of row mrow is the
           // lanes fr, fr + 16, fr + 32, fr + 48 (fg = 0..3): block amax by the two lane swaps;
           // bf16-rounded values, so the bytes equal vtd_quantize_mx8 of the bf16 output
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            v0[j] = bf16_round(v0[j]);
-            v1[j] = bf16_round(v1[j]);
-          }
+          bf16_round4(v0);
+          bf16_round4(v1);
           float am = 0.f;
 #pragma unroll
           for (int j = 0; j < 4; ++j) am = fmaxf(am, fmaxf(fabsf(v0[j]), fabsf(v1[j])));
