@@ -287,7 +287,11 @@ int vtd_fold_layernorm(const float* w32_dev, int N, int K, int ldw, const float*
 /* keras MultiHeadAttention core (vtd.py:364-369): per batch b, head h,
  * O = softmax(scale * Q K^T) V with Q, K, V read from qkv [B*N][ldqkv] at column
  * offsets h*dkp, inner + h*dkp, 2*inner + h*dkp (inner = heads*dkp); O written to
- * out [B*N][ldo] at column h*dkp.  dkp in {32, 64, 128}; scale = 1/sqrt(key_dim). */
+ * out [B*N][ldo] at column h*dkp.  dkp in {32, 64, 128}; scale = 1/sqrt(key_dim).
+ * dtype VTD_BF16X3 (the split-bf16 parity mode): qkv is fp32, every product runs as three
+ * bf16 MFMA products (hi.hi + lo.hi + hi.lo, fp32 softmax statistics), and out is the
+ * split-bf16 A operand of the attention-output Dense, [hi | lo | hi] in three ldo / 3 wide
+ * pieces (ldo % 3 == 0, ldo / 3 >= heads*dkp; columns [heads*dkp, ldo / 3) not written). */
 int vtd_attention(const void* qkv_dev, int B, int N, int heads, int dkp, int ldqkv,
                   float scale, void* out_dev, int ldo, int dtype, void* stream);
 

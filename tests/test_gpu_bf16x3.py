@@ -225,3 +225,58 @@ def test_split_arguments_validated(L, cuda):
     e = _epi(L, out, 190, L.BF16X3)
     assert L.lib.vtd_gemm(4, 64, 64, x.data_ptr(), 64, x.data_ptr(), 64, L.F32, ctypes.byref(e),
                           None) == -1            # split output needs bf16 operands
+
+
+def _attn_ref64(qkv, B, N, H, dk, dkp):
+    q = qkv[:, :H * dkp].reshape(B, N, H, dkp)[..., :dk]
+    k = qkv[:, H * dkp:2 * H * dkp].reshape(B, N, H, dkp)[..., :dk]
+    v = qkv[:, 2 * H * dkp:3 * H * dkp].reshape(B, N, H, dkp)[..., :dk]
+    s = np.einsum("bqhd,bkhd->bhqk", q, k) / math.sqrt(dk)
+    p = ref.softmax(s, axis=-1)
+    return np.einsum("bhqk,bkhd->bqhd", p, v)
+
+
+@pytest.mark.parametrize("B,N,H,dk", [(2, 196, 3, 64), (1, 70, 2, 40), (1, 1, 1, 32),
+                                      (1, 333, 2, 128), (2, 1600, 2, 64), (3, 576, 3, 64),
+                                      (40, 196, 12, 64), (1, 64, 4, 20), (1, 129, 2, 100)])
+def test_attention_split_vs_fp64(L, cuda, B, N, H, dk):
+    """vtd_attention with dtype VTD_BF16X3 (vtd.py:364-369 in the split-bf16 parity mode): f32
+    query / key / value in, every product as hi.hi + lo.hi + hi.lo on the bf16 MFMA with fp32
+    softmax statistics, the output written as the attention-output Dense's split-bf16 A operand
+    [hi | lo | hi].  hi + lo against the fp64 attention of the same f32 inputs: within 2e-5
+    of max |O| (the f32 kernel's bound in test_gpu_kernels.test_attention)."""
+    dkp = 32 if dk <= 32 else (64 if dk <= 64 else 128)
+    ld = 3 * H * dkp + 8
+    g = np.random.default_rng(N * 10 + dk)
+    qkv = np.zeros((B * N, ld), np.float32)
+    for part in range(3):
+        for h in range(H):
+            c0 = part * H * dkp + h * dkp
+            qkv[:, c0:c0 + dk] = g.normal(0, 1.5, size=(B * N, dk))
+    P = H * dkp + 64
+    out = torch.full((B * N, 3 * P), -1, dtype=torch.int16, device=cuda)
+    qkv_d = torch.from_numpy(qkv).to(cuda)
+    L.check(L.lib.vtd_attention(qkv_d.data_ptr(), B, N, H, dkp, ld, 1.0 / math.sqrt(dk),
+                                out.data_ptr(), 3 * P, L.BF16X3, L.stream_ptr()), "attention")
+    torch.cuda.synchronize()
+    got = as_u16(out)
+    inner = H * dkp
+    assert np.array_equal(got[:, 2 * P:2 * P + inner], got[:, :inner])   # third piece = hi
+    assert (got[:, inner:P] == 0xFFFF).all()                              # not written
+    hi = bf16_to_f32(got[:, :inner]).astype(np.float64)
+    lo = bf16_to_f32(got[:, P:P + inner]).astype(np.float64)
+    # the lo piece is the split of the f32 value hi + lo: |lo| <= half an ulp of bf16(hi)
+    assert (np.abs(lo) <= np.abs(hi) * 2.0 ** -7 + 1e-38).all()
+    o = (hi + lo).reshape(B, N, H, dkp)
+    exp = _attn_ref64(qkv.astype(np.float64), B, N, H, dk, dkp)
+    assert np.abs(o[..., :dk] - exp).max() < 2e-5 * max(1.0, np.abs(exp).max())
+    assert (o[..., dk:] == 0).all()
+
+
+def test_attention_split_arguments_validated(L, cuda):
+    x = torch.zeros(196, 3 * 64, device=cuda)
+    y = torch.zeros(196, 3 * 64 + 1, dtype=torch.int16, device=cuda)
+    assert L.lib.vtd_attention(x.data_ptr(), 1, 196, 1, 64, 192, 0.125, y.data_ptr(), 193,
+                               L.BF16X3, None) == -1        # ldo % 3 != 0
+    assert L.lib.vtd_attention(x.data_ptr(), 1, 196, 1, 64, 192, 0.125, y.data_ptr(), 96,
+                               L.BF16X3, None) == -1        # piece narrower than heads * dkp

@@ -23,17 +23,24 @@ def main():
     ap.add_argument("--flush", action="store_true", help="evict the MALL between reps")
     ap.add_argument("--variants", default="-1")
     ap.add_argument("--rounds", type=int, default=1)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32", "x3"],
+                    help="x3: the split-bf16 kernel (f32 qkv in, [hi | lo | hi] out)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     B, N, H, dkp = a.B, a.N, a.H, 64
     ld = 3 * H * dkp
     g = torch.Generator(device=dev).manual_seed(0)
-    qkv = (torch.randn(B * N, ld, generator=g, device=dev) * 1.5).to(torch.bfloat16)
-    out = torch.empty(B * N, H * dkp, device=dev, dtype=torch.bfloat16)
+    code = {"bf16": L.BF16, "f32": L.F32, "x3": L.BF16X3}[a.dtype]
+    qkv = torch.randn(B * N, ld, generator=g, device=dev) * 1.5
+    if a.dtype == "bf16":
+        qkv = qkv.to(torch.bfloat16)
+    ldo = 3 * H * dkp if a.dtype == "x3" else H * dkp
+    out = torch.empty(B * N, ldo, device=dev,
+                      dtype=torch.float32 if a.dtype == "f32" else torch.bfloat16)
     junk = torch.empty(512 << 20, dtype=torch.uint8, device=dev) if a.flush else None
     st = L.stream_ptr()
     call = lambda: L.check(L.lib.vtd_attention(qkv.data_ptr(), B, N, H, dkp, ld, 1 / math.sqrt(64),
-                                               out.data_ptr(), H * dkp, L.BF16, st))
+                                               out.data_ptr(), ldo, code, st))
     t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for rnd in range(a.rounds):
         for v in [int(x) for x in a.variants.split(",")]:
@@ -50,8 +57,8 @@ def main():
                     torch.cuda.synchronize()
                     ms += t0.elapsed_time(t1)
             us = 1e3 * ms / a.reps
-            byts = B * N * (ld + H * dkp) * 2
-            print(json.dumps({"variant": v, "round": rnd, "B": B, "N": N,
+            byts = B * N * (ld * qkv.element_size() + ldo * out.element_size())
+            print(json.dumps({"dtype": a.dtype, "variant": v, "round": rnd, "B": B, "N": N,
                               "flush": a.flush, "us": round(us, 2),
                               "hbm_tbs": round(byts / us / 1e6, 2),
                               "tflops": round(4.0 * B * H * N * N * 64 / us / 1e6, 1)}), flush=True)

@@ -1330,6 +1330,296 @@ int launch_bf16_fl(const void* qkv, int B, int N, int heads, int ldqkv, float sc
   return VTD_OK;
 }
 
+// ---------------------------------------------------------------------------------
+// Split-bf16 kernel (the VTD_BF16X3 parity mode; include/vtd.h "Split-bf16 operands").
+// Q, K, V arrive as f32 (the query/key/value GEMM's f32 output) and every product runs on
+// the bf16 MFMA as three: hi.hi + lo.hi + hi.lo with hi = bf16(v), lo = bf16(v - hi), fp32
+// accumulators -- S^T = K Q^T over (K_hi, K_lo) x (Q_hi, Q_lo) and O^T += V^T P^T over
+// (V_hi, V_lo) x (P_hi, P_lo), P in fp32 split the same way; the dropped lo.lo term is
+// <= 2^-18 of each product.  Softmax statistics stay fp32.  Structure as
+// attention_bf16_kernel (32 queries per wave, 64-key chunks register-staged from global
+// memory into one of two LDS buffers, one barrier per chunk, the deferred-rescale online
+// softmax); the split of K / V happens once per workgroup, in the staging write (hi and lo
+// planes with the bf16 kernel's row strides, so the K reads and the V^T tr-reads are the
+// bf16 kernel's).  The output is written directly as the attention_output GEMM's split-bf16
+// A operand [hi | lo | hi] (three P = ldo / 3 wide pieces), so no split pass follows it.
+template <int DKP>
+struct AttnX3Cfg {
+  static constexpr int KC = 64;                       // keys per chunk
+  static constexpr int KS = DKP * 2 + 16;             // K row stride (bytes, per plane)
+  static constexpr int VS = DKP * 2 + 64;             // V row stride (bytes, per plane)
+  static constexpr int PLANE = KC * KS + KC * VS;     // K then V image of one plane
+  static constexpr int BUF = 2 * PLANE;               // hi plane, lo plane
+  static constexpr int CPR = DKP / 4;                 // 16-B f32 chunks per row
+  static constexpr int NCH = KC * CPR * 2;            // chunks per K + V tile
+  static constexpr int KSTEPS = DKP / 16;
+  static constexpr int DB = DKP / 32;
+};
+
+// 8 f32 values -> split-bf16 (hi, lo) fragments
+__device__ __forceinline__ void split8(const f32x4& a, const f32x4& b, bf16x8& hi, bf16x8& lo) {
+  const uint32_t h0 = pack_bf16x2(a[0], a[1]), h1 = pack_bf16x2(a[2], a[3]);
+  const uint32_t h2 = pack_bf16x2(b[0], b[1]), h3 = pack_bf16x2(b[2], b[3]);
+  hi = __builtin_bit_cast(bf16x8, i32x4{(int)h0, (int)h1, (int)h2, (int)h3});
+  lo = __builtin_bit_cast(bf16x8, i32x4{(int)pack_lo_bf16x2(a[0], a[1], h0),
+                                        (int)pack_lo_bf16x2(a[2], a[3], h1),
+                                        (int)pack_lo_bf16x2(b[0], b[1], h2),
+                                        (int)pack_lo_bf16x2(b[2], b[3], h3)});
+}
+
+template <int DKP, int NWG>
+__global__ __launch_bounds__(64 * NWG, 1) void attention_x3_kernel(
+    const float* __restrict__ qkv, int N, int heads, int ldqkv, float scale_log2,
+    bf16_t* __restrict__ out, int ldo, int nqb) {
+  using C = AttnX3Cfg<DKP>;
+  typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  constexpr int nthreads = 64 * NWG;
+  const int lane = tid & 63, wave = tid >> 6, half = lane >> 5, col = lane & 31;
+  int v = blockIdx.x;                  // XCD-aware: a pair's query blocks share an XCD
+  {
+    const int G = gridDim.x, xcd = v & 7, q8 = G >> 3, r8 = G & 7;
+    v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (v >> 3);
+  }
+  const int pair = v / nqb, qb = v - pair * nqb;
+  const int b = pair / heads, h = pair - b * heads;
+  const int inner = heads * DKP;
+  const int64_t row0 = (int64_t)b * N;
+  const int q0 = (qb * NWG + wave) * 32;
+  const bool active = q0 < N;
+  const int P = ldo / 3;               // piece width of the split output
+
+  bf16x8 qh[C::KSTEPS], ql[C::KSTEPS];
+  {
+    const int q = min(q0 + col, N - 1);
+    const float* qp = qkv + (row0 + q) * ldqkv + h * DKP;
+#pragma unroll
+    for (int st = 0; st < C::KSTEPS; ++st)
+      split8(*reinterpret_cast<const f32x4*>(qp + st * 16 + half * 8),
+             *reinterpret_cast<const f32x4*>(qp + st * 16 + half * 8 + 4), qh[st], ql[st]);
+  }
+  f32x16 o[C::DB];
+#pragma unroll
+  for (int i = 0; i < C::DB; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+
+  constexpr int NPASS = (C::NCH + nthreads - 1) / nthreads;
+  f32x4 stg[NPASS];
+  auto gload = [&](int kv0) {
+#pragma unroll
+    for (int i = 0; i < NPASS; ++i) {
+      const int c = tid + i * nthreads;
+      if (c < C::NCH) {
+        const int isv = c >= C::KC * C::CPR;
+        const int cc = c - isv * C::KC * C::CPR;
+        const int kr = cc / C::CPR, ch = cc - kr * C::CPR;
+        const int key = min(kv0 + kr, N - 1);
+        stg[i] = *reinterpret_cast<const f32x4*>(qkv + (row0 + key) * ldqkv +
+                                                 (1 + isv) * inner + h * DKP + ch * 4);
+      }
+    }
+  };
+  // split once per workgroup: 4 f32 -> 8 B of the hi plane + 8 B of the lo plane
+  auto swrite = [&](int buf) {
+    char* base = smem + buf * C::BUF;
+#pragma unroll
+    for (int i = 0; i < NPASS; ++i) {
+      const int c = tid + i * nthreads;
+      if (c < C::NCH) {
+        const int isv = c >= C::KC * C::CPR;
+        const int cc = c - isv * C::KC * C::CPR;
+        const int kr = cc / C::CPR, ch = cc - kr * C::CPR;
+        char* dst = isv ? base + C::KC * C::KS + kr * C::VS + ch * 8 : base + kr * C::KS + ch * 8;
+        const uint32_t h0 = pack_bf16x2(stg[i][0], stg[i][1]), h1 = pack_bf16x2(stg[i][2], stg[i][3]);
+        *reinterpret_cast<uint2*>(dst) = uint2{h0, h1};
+        *reinterpret_cast<uint2*>(dst + C::PLANE) =
+            uint2{pack_lo_bf16x2(stg[i][0], stg[i][1], h0), pack_lo_bf16x2(stg[i][2], stg[i][3], h1)};
+      }
+    }
+  };
+
+  const int nchunks = (N + C::KC - 1) / C::KC;
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  const int tr_key = 4 * half + ((lane & 15) >> 2);
+  const int tr_d = ((lane >> 4) & 1) * 16 + (lane & 3) * 4;
+  auto chunk = [&](int c, auto last_tag) {
+    constexpr bool LAST = decltype(last_tag)::value;
+    const int kv0 = c * C::KC;
+    if (!LAST) gload(kv0 + C::KC);
+    if (active) {
+      const char* kl = smem + (c & 1) * C::BUF;      // hi plane; lo plane at + PLANE
+      const char* vl = kl + C::KC * C::KS;
+      const int nkb = LAST ? min(2, (N - kv0 + 31) >> 5) : 2;
+      const bool ragged = LAST && kv0 + C::KC > N;
+      f32x16 s[2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        if (kb < nkb) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+          const char* krow = kl + (kb * 32 + col) * C::KS;
+#pragma unroll
+          for (int st = 0; st < C::KSTEPS; ++st) {
+            const bf16x8 kh = *reinterpret_cast<const bf16x8*>(krow + (st * 16 + half * 8) * 2);
+            const bf16x8 klo =
+                *reinterpret_cast<const bf16x8*>(krow + C::PLANE + (st * 16 + half * 8) * 2);
+            s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, qh[st], s[kb], 0, 0, 0);
+            s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(klo, qh[st], s[kb], 0, 0, 0);
+            s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh, ql[st], s[kb], 0, 0, 0);
+          }
+        }
+      }
+      if (ragged) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kv0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+            if (key >= N) s[kb][r] = -INFINITY;
+          }
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+        if (kb < nkb) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
+        }
+      mx = pair_max(mx) * scale_log2;
+      // deferred rescale (attention_bf16_kernel): P <= 256, split exactly as any f32 value
+      if (__builtin_amdgcn_ballot_w64(mx > m_run + 8.f)) {
+        const float m_new = fmaxf(m_run, mx);
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        m_run = m_new;
+        l_run *= alpha;
+#pragma unroll
+        for (int i = 0; i < C::DB; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+      }
+      float ps0 = 0.f, ps1 = 0.f;
+      const float nm = -m_run;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+        if (kb < nkb) {
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            const float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][r], scale_log2, nm));
+            const float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][r + 1], scale_log2, nm));
+            s[kb][r] = p0;
+            s[kb][r + 1] = p1;
+            ps0 += p0;
+            ps1 += p1;
+          }
+        }
+      l_run += ps0 + ps1;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+        if (kb < nkb) {
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            bf16x8 ph, pl;
+            split8(f32x4{s[kb][8 * st + 0], s[kb][8 * st + 1], s[kb][8 * st + 2], s[kb][8 * st + 3]},
+                   f32x4{s[kb][8 * st + 4], s[kb][8 * st + 5], s[kb][8 * st + 6], s[kb][8 * st + 7]},
+                   ph, pl);
+            const int key0 = kb * 32 + 16 * st + tr_key;
+#pragma unroll
+            for (int db = 0; db < C::DB; ++db) {
+              const char* va = vl + key0 * C::VS + (db * 32 + tr_d) * 2;
+              const bf16x4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)va);
+              const bf16x4 h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(va + 8 * C::VS));
+              const bf16x4 l0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(va + C::PLANE));
+              const bf16x4 l1 =
+                  __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(va + C::PLANE + 8 * C::VS));
+              const bf16x8 vh = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+              const bf16x8 vlo = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+              o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, ph, o[db], 0, 0, 0);
+              o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vlo, ph, o[db], 0, 0, 0);
+              o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vh, pl, o[db], 0, 0, 0);
+            }
+          }
+        }
+    }
+    if (!LAST) swrite((c + 1) & 1);
+    __syncthreads();
+  };
+  for (int c = 0; c + 1 < nchunks; ++c) chunk(c, std::false_type{});
+  chunk(nchunks - 1, std::true_type{});
+  if (!active) return;
+  const float inv = 1.f / pair_sum(l_run);
+  if constexpr (DKP == 64) {
+    // restaged through the LDS free after the loop's last barrier: per wave a hi and a lo
+    // image of its 32 query rows (row stride 144 B), then whole 128-B rows per store
+    char* wst = smem + wave * (2 * 32 * 144);
+#pragma unroll
+    for (int db = 0; db < C::DB; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float a = o[db][4 * g + 0] * inv, bb = o[db][4 * g + 1] * inv;
+        const float cc = o[db][4 * g + 2] * inv, d = o[db][4 * g + 3] * inv;
+        const uint32_t h0 = pack_bf16x2(a, bb), h1 = pack_bf16x2(cc, d);
+        char* dst = wst + col * 144 + (db * 32 + 8 * g + 4 * half) * 2;
+        *reinterpret_cast<uint2*>(dst) = uint2{h0, h1};
+        *reinterpret_cast<uint2*>(dst + 32 * 144) =
+            uint2{pack_lo_bf16x2(a, bb, h0), pack_lo_bf16x2(cc, d, h1)};
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // wave-local: own writes landed
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {
+      const int r = pass * 8 + (lane >> 3), ch = lane & 7;
+      if (q0 + r < N) {
+        bf16_t* op = out + (row0 + q0 + r) * ldo + h * DKP + ch * 8;
+        const i32x4 hv = *reinterpret_cast<const i32x4*>(wst + r * 144 + ch * 16);
+        const i32x4 lv = *reinterpret_cast<const i32x4*>(wst + 32 * 144 + r * 144 + ch * 16);
+        *reinterpret_cast<i32x4*>(op) = hv;
+        *reinterpret_cast<i32x4*>(op + P) = lv;
+        *reinterpret_cast<i32x4*>(op + 2 * P) = hv;
+      }
+    }
+    return;
+  }
+  const int q = q0 + col;
+  if (q >= N) return;
+  bf16_t* op = out + (row0 + q) * ldo + h * DKP;
+#pragma unroll
+  for (int db = 0; db < C::DB; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d = db * 32 + 8 * g + 4 * half;
+      const float a = o[db][4 * g + 0] * inv, bb = o[db][4 * g + 1] * inv;
+      const float cc = o[db][4 * g + 2] * inv, dd = o[db][4 * g + 3] * inv;
+      const uint32_t h0 = pack_bf16x2(a, bb), h1 = pack_bf16x2(cc, dd);
+      const uint2 hv = {h0, h1}, lv = {pack_lo_bf16x2(a, bb, h0), pack_lo_bf16x2(cc, dd, h1)};
+      *reinterpret_cast<uint2*>(op + d) = hv;
+      *reinterpret_cast<uint2*>(op + P + d) = lv;
+      *reinterpret_cast<uint2*>(op + 2 * P + d) = hv;
+    }
+}
+
+template <int DKP>
+int launch_x3(const void* qkv, int B, int N, int heads, int ldqkv, float scale, void* out,
+              int ldo, hipStream_t stream) {
+  using C = AttnX3Cfg<DKP>;
+  constexpr int NWG = 8;
+  const int nq = (N + 31) / 32, nqb = (nq + NWG - 1) / NWG;
+  VTD_CHECK_ARG((int64_t)nqb * heads * B < INT32_MAX, "attention: grid too large");
+  static std::once_flag once[kMaxDevices];
+  once_per_device(once, [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_x3_kernel<DKP, NWG>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 2 * C::BUF);
+  });
+  hipLaunchKernelGGL((attention_x3_kernel<DKP, NWG>), dim3(nqb * heads * B), dim3(64 * NWG),
+                     2 * C::BUF, stream, static_cast<const float*>(qkv), N, heads, ldqkv,
+                     scale * 1.4426950408889634f, static_cast<bf16_t*>(out), ldo, nqb);
+  VTD_LAUNCH_CHECK("attention_x3");
+  return VTD_OK;
+}
+
 template <int DKP, int NWG, bool MX8 = false>
 int launch_bf16_v2(const void* qkv, int B, int N, int heads, int ldqkv, float scale,
                    void* out, int ldo, hipStream_t stream, uint8_t* s8 = nullptr,
@@ -1384,12 +1674,22 @@ int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqk
   VTD_CHECK_ARG(qkv && out, "attention: null pointer");
   VTD_CHECK_ARG(B > 0 && N > 0 && heads > 0, "attention: bad B/N/heads");
   VTD_CHECK_ARG(dkp == 32 || dkp == 64 || dkp == 128, "attention: dkp must be 32/64/128");
-  VTD_CHECK_ARG(ldqkv >= 3 * heads * dkp && ldo >= heads * dkp,
+  VTD_CHECK_ARG(dtype == VTD_F32 || dtype == VTD_BF16 || dtype == VTD_BF16X3,
+                "attention: bad dtype");
+  // VTD_BF16X3: f32 qkv in, the split-bf16 operand [hi | lo | hi] out (ldo = 3 P, P >= inner)
+  const int owidth = dtype == VTD_BF16X3 ? ldo / 3 : ldo;
+  VTD_CHECK_ARG(dtype != VTD_BF16X3 || ldo % 3 == 0,
+                "attention: a split-bf16 output needs ldo % 3 == 0");
+  VTD_CHECK_ARG(ldqkv >= 3 * heads * dkp && owidth >= heads * dkp,
                 "attention: leading dimensions too small");
-  VTD_CHECK_ARG(ldqkv % 8 == 0 && ldo % 8 == 0, "attention: ld must be multiple of 8");
-  VTD_CHECK_ARG(dtype == VTD_F32 || dtype == VTD_BF16, "attention: bad dtype");
+  VTD_CHECK_ARG(ldqkv % 8 == 0 && owidth % 8 == 0, "attention: ld must be multiple of 8");
   ProfScope ps(stream, PROF_ATTN,
                flops > 0 ? flops : 4.0 * B * heads * (double)N * N * dkp);
+  if (dtype == VTD_BF16X3) {
+    if (dkp == 32) return launch_x3<32>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+    if (dkp == 64) return launch_x3<64>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+    return launch_x3<128>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+  }
   if (dtype == VTD_BF16) {
     // knob VTD_KNOB_ATTN_VARIANT (environment read once per process; tests set it per call)
     const int kv = knob(VTD_KNOB_ATTN_VARIANT);

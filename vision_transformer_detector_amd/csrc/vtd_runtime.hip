@@ -270,8 +270,9 @@ Plan make_plan(const vtd_config* c, const vtd_dims& d, int nparts = 1) {
   p.stat = take(R * 8);                 // LayerNorm (mean, rstd) per row, fold path
   p.pstat = take(R * (d.d_p / 64) * 8);  // producer partial (sum, sumsq) per 64 columns
   p.qkv = take(R * d.qkv_p * es);
-  p.attn = take(R * d.inner_p * es);
-  // VTD_BF16X3: the attention output as the split-bf16 operand of attention_output
+  // the attention output; VTD_BF16X3: written by the attention kernel as the split-bf16
+  // operand of attention_output (attn3), no f32 copy
+  p.attn = take(c->dtype == VTD_BF16X3 ? 0 : R * d.inner_p * es);
   p.attn3 = take(c->dtype == VTD_BF16X3 ? R * d.inner_p * eop : 0);
   p.mlp0 = take(R * mlp_max * eop);
   p.mlp1 = take(R * mlp_max * eop);
@@ -628,9 +629,9 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     VTD_HIP(hipMemsetAsync(static_cast<char*>(patches) + (size_t)d.rows * row_bytes, 0,
                            (size_t)(R - d.rows) * row_bytes, st));
     // and the attention output's pad rows, which the attention never writes
-    const size_t attn_row = (size_t)d.inner_p * es_of(cfg->dtype);
-    VTD_HIP(hipMemsetAsync(static_cast<char*>(attn) + (size_t)d.rows * attn_row, 0,
-                           (size_t)(R - d.rows) * attn_row, st));
+    const size_t attn_row = (size_t)d.inner_p * (x3 ? eop_of(cfg->dtype) : es_of(cfg->dtype));
+    VTD_HIP(hipMemsetAsync(static_cast<char*>(x3 ? ws + P.attn3 : attn) + (size_t)d.rows * attn_row,
+                           0, (size_t)(R - d.rows) * attn_row, st));
   }
   // ---- linear_projection + position embedding add (vtd.py:291-307)
   {
@@ -683,17 +684,13 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     rc = diag_noattn ? VTD_OK
          : attn_mx8 ? attention_mx8_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale,
                                          q8, d.inner_p, s8, P.s8_rows, st, attn_flops)
+         : x3 ? attention_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale,
+                                 ws + P.attn3, kk(d.inner_p), VTD_BF16X3, st, attn_flops, nparts)
                   : attention_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale,
                                      attn, d.inner_p, dt, st, attn_flops, nparts);
     if (rc) return rc;
-    // VTD_BF16X3: the f32 attention output split into the attention_output GEMM's operand
-    const void* attn_op = attn;
-    if (x3) {
-      rc = split_bf16x3_launch(static_cast<const float*>(attn), R, d.inner_p, d.inner_p,
-                               ws + P.attn3, kk(d.inner_p), 0, st);
-      if (rc) return rc;
-      attn_op = ws + P.attn3;
-    }
+    // VTD_BF16X3: the attention wrote the attention_output GEMM's split-bf16 operand itself
+    const void* attn_op = x3 ? ws + P.attn3 : attn;
     {
       vtd_epilogue e{};
       e.bias = L.b_out; e.act = VTD_ACT_NONE;
