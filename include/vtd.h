@@ -377,7 +377,8 @@ int vtd_png_inflate(const uint8_t* png, size_t len, uint8_t* out, size_t out_byt
  * (decode_image_op.cc): the file's channels = bits-per-pixel / 8 in {1, 3, 4}, rows bottom-up
  * (top-down for a negative height) padded to 4 bytes; 24-bit BGR -> RGB, 32-bit BGRA -> RGB
  * (alpha dropped), 8-bit -> the stored byte replicated (TF applies no palette).  Other bit
- * depths and RLE compression (which TF would misread) return VTD_ERR_UNSUPPORTED.  Same
+ * depths and any compression but BI_RGB / BI_BITFIELDS (RLE, BI_JPEG, BI_PNG: bytes TF would
+ * misread as pixels) return VTD_ERR_UNSUPPORTED.  Same
  * calling convention as the PNG / JPEG entry points; comps = 3. */
 int vtd_bmp_info(const uint8_t* bmp, size_t len, int* h, int* w, int* comps);
 int vtd_bmp_workspace_bytes(const uint8_t* const* bmps, const size_t* lens, int n,

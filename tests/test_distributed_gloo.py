@@ -100,7 +100,7 @@ def test_data_parallel_gather_matches_single_process(world, batch):
         assert (kern == 10.0).all()            # everyone now holds rank 0's weights
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_bench_launches_ranks_itself(world):
     """`python bench.py --gpus N` with no launcher starts N rank processes (the driver's
     command shape); --dry-run rehearses the rendezvous, max-over-ranks timing and the
@@ -123,6 +123,36 @@ def test_bench_launches_ranks_itself(world):
     # correctness evidence of the N > 1 line: each rank finds its own shard in the gather
     assert out["gather_ok"] is True
     assert 0 <= out["rank_ms_min"] <= out["rank_ms_max"]
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_under_the_drivers_launcher(world):
+    """The driver's N > 1 command shape: `python -m torch.distributed.run --nnodes=1
+    --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...`
+    (WORLD_SIZE / RANK from the launcher), rehearsed with --dry-run on gloo."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", str(world), "--master-addr", "127.0.0.1",
+                        "--master-port", str(port), os.path.join(root, "bench.py"),
+                        "--gpus", str(world), "--dry-run", "--steps", "3", "--warmup", "1",
+                        "--batch", "5"], capture_output=True, text=True, timeout=240, env=env,
+                       cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == world and out["config"]["global_batch"] == 5 * world
+    assert out["gather_rank_order_ok"] is True and out["gather_ok"] is True
 
 
 def test_bench_rejects_gpus_world_mismatch():

@@ -55,6 +55,20 @@ def test_tiny_golden(vtd, cuda, name, dtype):
         assert np.abs(d.cpu().numpy() - dets).max() < 1e-3 * 608
 
 
+def test_default_dtype_is_the_split_bf16_parity_mode(vtd, cuda):
+    """The drop-in default (no `dtype` kwarg, as a caller swapping the reference's import
+    would build it) is the split-bf16 mode, within 1e-4 of the fp64 oracle (the reference is
+    fp32 throughout, vtd.py:297-493)."""
+    from vision_transformer_detector_amd import _lib as L
+    kw, w, x, logits, _ = load_tiny("tiny_gelu")
+    model = vtd.create_vision_transformer_detector(**kw)
+    assert model.dtype == L.BF16X3
+    model.set_weights(w)
+    ok, rel = within(model(torch.from_numpy(x).to(cuda), training=False).cpu().numpy(), logits,
+                     TOL["bf16x3"])
+    assert ok, f"default dtype: max rel err {rel:.3e}"
+
+
 @pytest.mark.parametrize("dtype", ["float32", "bf16x3", "bfloat16", "float8"])
 @pytest.mark.parametrize("batch", [1, 5])
 def test_fused_decode_equals_transform_predictions(vtd, cuda, dtype, batch):

@@ -258,3 +258,19 @@ def test_bench_golden_generators_match_oracle():
                           V.synthetic_images(3, (40, 36, 3), seed=4, letterbox=True))
     spec = json.load(open(os.path.join(ROOT, "tests", "golden", "batched_forward.json")))
     assert bench.GOLDEN_CASE in spec and len(bench.GOLDEN_POS) == spec[bench.GOLDEN_CASE]["n"]
+
+
+def test_enable_device_kernel_arguments_reports_effect(monkeypatch):
+    """The opt-in kernel-argument placement takes effect only before the HIP runtime
+    initialises: after it, the helper says so (False + a warning) instead of claiming it."""
+    import torch
+    import vision_transformer_detector_amd as vtd
+    monkeypatch.delenv("HIP_FORCE_DEV_KERNARG", raising=False)
+    monkeypatch.setattr(torch.cuda, "is_initialized", lambda: True)
+    with pytest.warns(RuntimeWarning, match="already initialised"):
+        assert vtd.enable_device_kernel_arguments() is False
+    assert "HIP_FORCE_DEV_KERNARG" not in os.environ
+    monkeypatch.setattr(torch.cuda, "is_initialized", lambda: False)
+    assert vtd.enable_device_kernel_arguments() is True
+    monkeypatch.setenv("HIP_FORCE_DEV_KERNARG", "0")        # an explicit setting wins
+    assert vtd.enable_device_kernel_arguments() is False

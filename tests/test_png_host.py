@@ -103,6 +103,15 @@ def test_bmp_header_and_refusals(L):
     g[30:34] = (1).to_bytes(4, "little")                       # BI_RLE8
     assert L.lib.vtd_bmp_info(bytes(g), len(g), ctypes.byref(h), ctypes.byref(w), ctypes.byref(c)) != 0
     assert b"RLE" in L.lib.vtd_last_error()
+    for comp in (4, 5, 6):                                     # BI_JPEG, BI_PNG, other
+        g = bytearray(f)
+        g[30:34] = comp.to_bytes(4, "little")
+        assert L.lib.vtd_bmp_info(bytes(g), len(g), ctypes.byref(h), ctypes.byref(w),
+                                  ctypes.byref(c)) != 0, comp
+        assert b"compression" in L.lib.vtd_last_error()
+    g = bytearray(f)
+    g[30:34] = (3).to_bytes(4, "little")                       # BI_BITFIELDS decodes
+    assert L.lib.vtd_bmp_info(bytes(g), len(g), ctypes.byref(h), ctypes.byref(w), ctypes.byref(c)) == 0
     assert L.lib.vtd_bmp_info(f[:60], 60, ctypes.byref(h), ctypes.byref(w), ctypes.byref(c)) != 0
     assert b"truncated" in L.lib.vtd_last_error()
 
@@ -120,6 +129,11 @@ def test_png_wide_rows_accepted(L):
     ihdr = _chunk(b"IHDR", struct.pack(">IIBBBBB", 1 << 15, (1 << 13) + 1, 8, 2, 0, 0, 0))
     f = sig + ihdr + _chunk(b"IEND", b"")
     assert _info(L, f)[0] != 0 and b"2^28" in L.lib.vtd_last_error()
+    # a one-row RGBA16 image of 2^28 pixels: 2^31 bytes per row (the unfilter kernel's int
+    # row index would wrap) -- refused, not decoded
+    ihdr = _chunk(b"IHDR", struct.pack(">IIBBBBB", 1 << 28, 1, 16, 6, 0, 0, 0))
+    f = sig + ihdr + _chunk(b"IEND", b"")
+    assert _info(L, f)[0] != 0 and b"2^31" in L.lib.vtd_last_error()
 
 
 def test_decode_images_routes_by_signature():

@@ -15,8 +15,17 @@ def enable_device_kernel_arguments() -> bool:
     kernel of the process receives its arguments and is read once, when the HIP runtime
     initialises, so call this before anything touches the GPU (bench.py and
     __graft_entry__.smoke do); an explicit HIP_FORCE_DEV_KERNARG setting wins.  Returns
-    whether the setting is now on.  VTD_DEV_KERNARG=1 in the environment does the same at
-    import time."""
+    whether the setting takes effect in this process: False (with a warning) when the HIP
+    runtime is already initialised here (e.g. after an earlier torch.cuda call), or when the
+    environment already says otherwise.  VTD_DEV_KERNARG=1 in the environment does the same
+    at import time."""
+    import sys
+    import warnings
+    torch = sys.modules.get("torch")
+    if torch is not None and torch.cuda.is_initialized():
+        warnings.warn("enable_device_kernel_arguments(): the HIP runtime is already initialised "
+                      "in this process; HIP_FORCE_DEV_KERNARG has no effect now", RuntimeWarning)
+        return False
     _os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
     return _os.environ["HIP_FORCE_DEV_KERNARG"] == "1"
 

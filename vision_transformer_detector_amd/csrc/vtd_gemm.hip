@@ -1862,7 +1862,7 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
     const bf16_t* b16 = static_cast<const bf16_t*>(Bt);
     const int ngw = tile_group_width(tiles_n);
 #if VTD_DIAG
-    if (gemm_variant() == 12) {
+    if (gemm_variant() == 12 && epi->out_dtype != VTD_BF16X3) {   // (w4: no split output)
       if (!gemm_w4_launch(M, N, K, a16, lda, b16, ldb, epi, ngw, stream))
         return fail(VTD_ERR_HIP, "gemm: w4 kernel attributes could not be set");
       VTD_LAUNCH_CHECK("gemm");

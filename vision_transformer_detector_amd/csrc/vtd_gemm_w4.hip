@@ -950,6 +950,8 @@ int x4_sched() {
 // LayerNorm partials into epi->lnstat).  Returns false when it does not apply.
 bool gemm_w4_launch(int M, int N, int K, const bf16_t* A, int lda, const bf16_t* Bt, int ldb,
                     const vtd_epilogue* epi, int ngw, hipStream_t stream) {
+  // no split-bf16 (VTD_BF16X3) output epilogue here: the caller's pp2 path writes it
+  if (epi->out_dtype == VTD_BF16X3) return false;
   EpiArgs e = make_epi_args(epi);
   e.ngw = ngw;
   auto a16 = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };

@@ -221,6 +221,11 @@ bool parse_png(const uint8_t* b, size_t n, PngDesc& d, std::vector<std::pair<siz
       if (!ok) { err = "png: invalid colour type / bit depth combination"; return false; }
       d.channels = ct == 0 ? 1 : ct == 2 ? 3 : ct == 3 ? 1 : ct == 4 ? 2 : 4;
       d.bpp = std::max(1, d.channels * d.depth / 8);
+      // the widest pass (the full width) indexes its row with int in the unfilter kernel
+      if (row_bytes(d.w, d.channels, d.depth) > (int64_t)INT32_MAX - kPngThreads - 1) {
+        err = "png: row wider than 2^31 bytes";
+        return false;
+      }
       ihdr = true;
     } else if (!ihdr) {
       err = "png: first chunk is not IHDR";
@@ -445,8 +450,8 @@ extern "C" int vtd_png_decode(const uint8_t* const* pngs, const size_t* lens, in
 // rows unless the height is negative, and converts to the 3 requested channels: 8-bit -> the
 // byte replicated (the palette is NOT applied), 24-bit BGR -> RGB, 32-bit BGRA -> RGB (alpha
 // dropped).  The compression field is not read by TF; here BI_RGB (0) and BI_BITFIELDS (3)
-// files decode that way and RLE files (1, 2), whose bytes TF would misread as pixels, are
-// refused.  TF is not importable here: parity against it is unpinned (restated from that
+// files decode that way and every other value (RLE 1 / 2, BI_JPEG 4, BI_PNG 5, ...), whose
+// bytes TF would misread as pixels, is refused.  TF is not importable here: parity against it is unpinned (restated from that
 // source).  The host reads the header; the pixel array goes to the workspace in one copy and
 // bmp_convert_kernel (one thread per output pixel) writes the RGB8 rows.
 namespace vtd {
@@ -492,9 +497,12 @@ bool parse_bmp(const uint8_t* b, size_t n, BmpDesc& d, int64_t& pix_off, std::st
           "files (channels = bits-per-pixel / 8 in 1, 3, 4)";
     return false;
   }
-  if (comp == 1 || comp == 2) {
-    err = "bmp: RLE-compressed BMP files are not supported (TF's decoder reads every file as "
-          "uncompressed rows)";
+  if (comp != 0 && comp != 3) {      // BI_RGB, BI_BITFIELDS (the default masks) only
+    err = comp == 1 || comp == 2
+              ? "bmp: RLE-compressed BMP files are not supported (TF's decoder reads every file "
+                "as uncompressed rows)"
+              : "bmp: compression " + std::to_string(comp) + " (BI_JPEG / BI_PNG / other) is not "
+                "supported: only uncompressed rows (BI_RGB, BI_BITFIELDS) decode";
     return false;
   }
   if (w <= 0 || h == 0 || h == INT32_MIN) { err = "bmp: bad size"; return false; }

@@ -392,9 +392,12 @@ SideStream* side_stream(hipStream_t st) {
 // Stages of one forward: 0 = patches + linear projection, 1..L = encoder layer s - 1,
 // L + 1 = head + decode.  forward_impl runs stages [s_lo, s_hi); `partials` carries
 // "the GEMM that last wrote x emitted LayerNorm partials" from one stage to the next.
+// nparts: the micro-batch parts of the forward (workspace plan, row padding, head split-K);
+// nconc: how many of them run concurrently (nparts, or 1 when they run one after another on
+// the caller's stream: a first call under graph capture) -- the persistent attention's grid
 int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* images,
                  float* logits, float* dets, char* ws, hipStream_t st, int s_lo, int s_hi,
-                 bool& partials, int nparts);
+                 bool& partials, int nparts, int nconc);
 }  // namespace
 
 }  // namespace vtd
@@ -447,7 +450,7 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
   if (!side) {
     bool partials = false;
     if (ns == 1)
-      return forward_impl(cfg, w, images, logits, dets, ws, st, 0, n_stages, partials, 1);
+      return forward_impl(cfg, w, images, logits, dets, ws, st, 0, n_stages, partials, 1, 1);
     // no side stream (first call under capture): the halves run in order on `st`
   }
   const size_t img = (size_t)cfg->image_h * cfg->image_w * cfg->channels;
@@ -508,7 +511,7 @@ int vtd_forward(const vtd_config* cfg, const vtd_weights* w, const float* images
       const int s = part == 0 ? t : t - stagger;
       if (s < 0 || s >= n_stages) continue;
       rc = forward_impl(&P.cfg, w, P.images, P.logits, P.dets, P.ws, P.st, s, s + 1, P.partials,
-                        ns);
+                        ns, side ? ns : 1);
       if (rc) return rc;
     }
   }
@@ -526,7 +529,7 @@ namespace vtd {
 namespace {
 int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* images,
                  float* logits, float* dets, char* ws, hipStream_t st, int s_lo, int s_hi,
-                 bool& partials, int nparts) {
+                 bool& partials, int nparts, int nconc) {
   vtd_dims d;
   int rc = derive(cfg, &d);
   if (rc) return rc;
@@ -685,9 +688,9 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
          : attn_mx8 ? attention_mx8_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale,
                                          q8, d.inner_p, s8, P.s8_rows, st, attn_flops)
          : x3 ? attention_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale,
-                                 ws + P.attn3, kk(d.inner_p), VTD_BF16X3, st, attn_flops, nparts)
+                                 ws + P.attn3, kk(d.inner_p), VTD_BF16X3, st, attn_flops, nconc)
                   : attention_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale,
-                                     attn, d.inner_p, dt, st, attn_flops, nparts);
+                                     attn, d.inner_p, dt, st, attn_flops, nconc);
     if (rc) return rc;
     // VTD_BF16X3: the attention wrote the attention_output GEMM's split-bf16 operand itself
     const void* attn_op = x3 ? ws + P.attn3 : attn;
