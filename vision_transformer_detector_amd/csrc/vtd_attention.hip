@@ -288,20 +288,46 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
   const int q0 = (qb * NWG + wave) * 32;
   const bool active = q0 < N;
 
+  // Q pre-scaled by scale * log2(e) (keras scales the query by 1 / sqrt(key_dim) before
+  // Q K^T [upstream]; the log2(e) factor makes the scores log2 units) and rounded to bf16
+  // again: a score is then exp2'ed as it leaves the MFMA, with no per-score multiply
   bf16x8 qf[C::KSTEPS];
   {
     const int q = min(q0 + col, N - 1);
     const bf16_t* qp = qkv + (row0 + q) * ldqkv + h * DKP;
 #pragma unroll
-    for (int st = 0; st < C::KSTEPS; ++st)
-      qf[st] = *reinterpret_cast<const bf16x8*>(qp + st * 16 + half * 8);
+    for (int st = 0; st < C::KSTEPS; ++st) {
+      const i32x4 raw = *reinterpret_cast<const i32x4*>(qp + st * 16 + half * 8);
+      i32x4 sc;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        sc[j] = (int)pack_bf16x2(__uint_as_float((uint32_t)raw[j] << 16) * scale_log2,
+                                 __uint_as_float((uint32_t)raw[j] & 0xffff0000u) * scale_log2);
+      qf[st] = __builtin_bit_cast(bf16x8, sc);
+    }
   }
   f32x16 o[C::DB];
 #pragma unroll
   for (int i = 0; i < C::DB; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
-  float m_run = -INFINITY, l_run = 0.f;
+  // Running max m_run (log2 units, kept exactly representable in bf16) subtracted INSIDE the
+  // score MFMA chain: one extra K-step multiplies the constant A column e_0 (1 at k = 0) by the
+  // B column -m_run (k = 0), so each score leaves the matrix core as s - m_run and P is one
+  // v_exp_f32 of it.  m_run starts at 0 and is set from the first chunk's max (`first`).
+  // SUMMFMA (dkp <= 64: register room): the row sum l rides in the PV MFMAs as a 32-row block
+  // of ones in V^T (every row of osum = sum_k P[k][q] of the bf16 P actually used), instead
+  // of one VALU add per score; otherwise l_run sums the fp32 P.
+  constexpr bool SUMMFMA = DKP <= 64;
+  float m_run = 0.f, l_run = 0.f;
+  const bf16_t one_bf16 = 0x3F80;
+  const bf16x8 a_e0 = {(short)(half == 0 ? one_bf16 : 0), 0, 0, 0, 0, 0, 0, 0};
+  const bf16x8 a_ones = {(short)one_bf16, (short)one_bf16, (short)one_bf16, (short)one_bf16,
+                         (short)one_bf16, (short)one_bf16, (short)one_bf16, (short)one_bf16};
+  bf16x8 b_m = {0, 0, 0, 0, 0, 0, 0, 0};        // -m_run at k = 0 (half 0 lanes)
+  f32x16 osum;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) osum[r] = 0.f;
 
   constexpr int NPASS = (C::NCH + nthreads - 1) / nthreads;
   i32x4 stg[NPASS];
@@ -356,12 +382,12 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
       const int nkb = LAST ? min(2, (N - kv0 + 31) >> 5) : 2;
       const bool ragged = LAST && kv0 + C::KC > N;
       f32x16 s[2];
+      const f32x16 zero = {};
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         if (kb < nkb) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
           const char* krow = kl + (kb * 32 + col) * C::KS;
+          s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_e0, b_m, zero, 0, 0, 0);   // -m_run
 #pragma unroll
           for (int st = 0; st < C::KSTEPS; ++st)
             s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
@@ -369,7 +395,7 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
                 s[kb], 0, 0, 0);
         }
       }
-      // raw-score max; scores beyond N (ragged last chunk only) are -inf
+      // scores beyond N (ragged last chunk only) are -inf
       if (ragged) {
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
@@ -386,40 +412,50 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
 #pragma unroll
           for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
         }
-      mx = pair_max(mx) * scale_log2;                  // lane l ^ 32 holds the other keys
-      // deferred rescale (running max in log2 units): the accumulators are rescaled only
-      // when some lane's max grows by more than 8, so exp2 arguments stay <= 8 (P <= 256,
-      // exact in the bf16 P operand's range, l and O in fp32); the final 1/l normalises
-      // whatever max was used consistently for O and l
-      if (__builtin_amdgcn_ballot_w64(mx > m_run + 8.f)) {
-        const float m_new = fmaxf(m_run, mx);
-        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+      mx = pair_max(mx);              // (relative to m_run) lane l ^ 32 holds the other keys
+      // deferred rescale: the accumulators are rescaled only when some lane's max grows by
+      // more than 8 (log2 units), so exp2 arguments stay <= 8 + 1/8 (P <= 2^8.125, exact in the
+      // bf16 P operand's range, l and O in fp32); the final 1/l normalises whatever max was
+      // used consistently for O and l.  The first chunk always sets the max.
+      if (__builtin_amdgcn_ballot_w64(c == 0 || mx > 8.f)) {
+        const float m_new = bf16_round(m_run + (c == 0 ? mx : fmaxf(mx, 0.f)));
+        const float dlt = m_new - m_run;
+        // (first chunk: O and l are still 0; dlt may be any size there)
+        const float alpha = c == 0 ? 0.f : __builtin_amdgcn_exp2f(-dlt);
         m_run = m_new;
+        b_m[0] = (short)(half == 0 ? f32_to_bf16(-m_new) : 0);
         l_run *= alpha;
+        osum[0] *= alpha;
 #pragma unroll
         for (int i = 0; i < C::DB; ++i)
 #pragma unroll
           for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) s[kb][r] -= dlt;
       }
-      // scalar fp32 VALU (v_fma_f32 / v_add_f32; the file is built without SLP packing):
-      // packed f32 ops cost more issue cycles beside MFMAs than two scalar ones; even / odd
-      // scores summed apart
-      float ps0 = 0.f, ps1 = 0.f;
-      const float nm = -m_run;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
         if (kb < nkb) {
 #pragma unroll
-          for (int r = 0; r < 16; r += 2) {
-            const float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][r], scale_log2, nm));
-            const float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(s[kb][r + 1], scale_log2, nm));
-            s[kb][r] = p0;
-            s[kb][r + 1] = p1;
-            ps0 += p0;
-            ps1 += p1;
-          }
+          for (int r = 0; r < 16; ++r) s[kb][r] = __builtin_amdgcn_exp2f(s[kb][r]);
         }
-      l_run += ps0 + ps1;
+      if constexpr (!SUMMFMA) {
+        // scalar fp32 adds (the file is built without SLP packing: packed f32 ops cost more
+        // issue cycles beside MFMAs than two scalar ones); even / odd scores summed apart
+        float ps0 = 0.f, ps1 = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+          if (kb < nkb) {
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+              ps0 += s[kb][r];
+              ps1 += s[kb][r + 1];
+            }
+          }
+        l_run += ps0 + ps1;
+      }
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
         if (kb < nkb) {
@@ -440,6 +476,7 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
               const bf16x8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
               o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb, o[db], 0, 0, 0);
             }
+            if constexpr (SUMMFMA) osum = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_ones, pb, osum, 0, 0, 0);
           }
         }
     }
@@ -449,7 +486,8 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
   for (int c = 0; c + 1 < nchunks; ++c) chunk(c, std::false_type{});
   chunk(nchunks - 1, std::true_type{});
   if (!active) return;
-  const float inv = 1.f / pair_sum(l_run);
+  // osum rows hold the whole key sum (both lane halves' keys); l_run holds this half's
+  const float inv = 1.f / (SUMMFMA ? osum[0] : pair_sum(l_run));
   const int q = q0 + col;
   if constexpr (!MX8 && DKP == 64) {
     // bf16 output through LDS (free after the loop's last barrier): a lane holds 16-B
