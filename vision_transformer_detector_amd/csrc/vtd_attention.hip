@@ -1040,273 +1040,6 @@ __global__ __launch_bounds__(64 * NW, 4) void attention_bf16_fl_kernel(
 }
 
 // ---------------------------------------------------------------------------------
-// Long-sequence ping-pong kernel (bf16, DKP = 64, N > 256: C3 N = 1600, C5 N = 576; knob
-// VTD_KNOB_ATTN_VARIANT 7).  One workgroup = 8 waves x 32 queries of one (image, head), in
-// two groups of 4 waves that run one workgroup barrier apart, like the pp2 GEMM: while one
-// group is in its MFMA phase the other is in its softmax (VALU) phase, so each SIMD holds one
-// wave of each and the matrix core runs one wave's products while the other wave's
-// exponentials issue.  Per 64-key chunk c a wave runs
-//   M(c): K(c) fragments from LDS; O^T += V^T P^T of chunk c - 1 (+ the row sum as a block of
-//         ones, see attention_bf16_kernel); S^T = K Q^T of chunk c (-m_run inside the chain)
-//   V(c): ragged mask, row max, deferred rescale, P(c) = exp2(S^T) as bf16; V(c)^T fragments
-//         (tr-reads, held in registers until M(c + 1)); the DMA of chunk c + NS - 1
-// with one barrier after each phase: G0's M(c) follows event 2c, G1's event 2c + 1.  K and V
-// chunks arrive by LDS-DMA (buffer_load ... lds; wave w one 8-row group of K and of V) into a
-// ring of NS = 4 slots of 16 KiB, NS - 1 chunks ahead (the fl kernel's swizzled images).
-// Slot of chunk j - 1 is last read in V(j - 1) (G1: until event 2j + 1, tr-reads retired by
-// lgkmcnt(0) before it); chunk j + NS - 1 overwrites it from V(j) (G0: after event 2j + 1).
-// RAW: chunk c + 1 must have landed by event 2c + 2: G0 waits at the end of V(c), G1 at the
-// end of M(c), each for its own pieces (counted vmcnt), then the barrier publishes them.
-// Arithmetic per score and output epilogues as attention_bf16_kernel (Q pre-scaled to log2
-// units, -m_run in the score MFMA chain, bf16-exact running max, ones-block row sum).
-template <bool MX8>
-__global__ __launch_bounds__(512, 1) void attention_bf16_pp_kernel(
-    const bf16_t* __restrict__ qkv, int N, int heads, int ldqkv, float scale_log2,
-    bf16_t* __restrict__ out, int ldo, uint8_t* __restrict__ s8, int64_t s_rows, int nqb) {
-  constexpr int DKP = 64, KC = 64, SLOT = 2 * KC * 128, NS = 4;
-  typedef __attribute__((address_space(3))) void lds_void_t;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = wave >> 2;
-  const int lane = tid & 63, half = lane >> 5, col = lane & 31;
-  int v = blockIdx.x;                         // XCD-aware: a pair's query blocks share an XCD
-  {
-    const int G = gridDim.x, xcd = v & 7, q8 = G >> 3, r8 = G & 7;
-    v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (v >> 3);
-  }
-  const int pair = v / nqb, qb = v - pair * nqb;
-  const int b = pair / heads, h = pair - b * heads;
-  const int inner = heads * DKP;
-  const int64_t row0 = (int64_t)b * N;
-  const int q0 = (qb * 8 + wave) * 32;
-  const bool active = q0 < N;
-  const uint32_t lds_base =
-      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(smem);
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16_t*>(qkv + row0 * ldqkv), 0, N * ldqkv * 2, 0x00020000);
-  const int lrow = lane >> 3, lchunk = lane & 7;
-  const int colk = (inner + h * DKP) * 2, colv = (2 * inner + h * DKP) * 2;
-  const int nch = (N + KC - 1) / KC;
-
-  // Q fragments first (the compiler's wait for them then leaves the ring's DMAs in flight),
-  // pre-scaled by scale * log2(e) and rounded to bf16 (attention_bf16_kernel)
-  bf16x8 qf[4];
-  {
-    const int q = min(q0 + col, N - 1);
-    const bf16_t* qp = qkv + (row0 + q) * ldqkv + h * DKP;
-#pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      const i32x4 raw = *reinterpret_cast<const i32x4*>(qp + st * 16 + half * 8);
-      i32x4 sc;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        sc[j] = (int)pack_bf16x2(__uint_as_float((uint32_t)raw[j] << 16) * scale_log2,
-                                 __uint_as_float((uint32_t)raw[j] & 0xffff0000u) * scale_log2);
-      qf[st] = __builtin_bit_cast(bf16x8, sc);
-    }
-  }
-  auto issue = [&](int c) {                   // chunk c: this wave's K and V row groups
-    char* dst = smem + (c % NS) * SLOT;
-    const int r = wave * 8 + lrow;
-    const int base = min(c * KC + r, N - 1) * ldqkv * 2;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + wave * 1024), 16,
-                                             base + colk + ((lchunk ^ swz_kq(r)) << 4), 0, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(dst + KC * 128 + wave * 1024), 16,
-                                             base + colv + ((lchunk ^ swz_v(r)) << 4), 0, 0, 0);
-  };
-  // counted wait: at most n of this wave's DMA pieces outstanding (n even, <= 4)
-  auto vm_wait_n = [](int n) {
-    if (n <= 0) vm_wait<0>();
-    else if (n <= 2) vm_wait<2>();
-    else vm_wait<4>();
-  };
-  for (int c = 0; c < NS - 1 && c < nch; ++c) issue(c);
-  vm_wait_n(2 * min(NS - 2, nch - 1));
-  __builtin_amdgcn_s_barrier();               // event 0: chunk 0 in LDS
-  if (grp == 1) __builtin_amdgcn_s_barrier(); // event 1: G1 one phase behind
-
-  f32x16 o[2], osum, s[2];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) o[0][r] = o[1][r] = osum[r] = 0.f;
-  float m_run = 0.f;
-  const bf16_t one_bf16 = 0x3F80;
-  const bf16x8 a_e0 = {(short)(half == 0 ? one_bf16 : 0), 0, 0, 0, 0, 0, 0, 0};
-  const bf16x8 a_ones = {(short)one_bf16, (short)one_bf16, (short)one_bf16, (short)one_bf16,
-                         (short)one_bf16, (short)one_bf16, (short)one_bf16, (short)one_bf16};
-  bf16x8 b_m = {0, 0, 0, 0, 0, 0, 0, 0};
-  const f32x16 zero = {};
-  bf16x8 pb[2][2];                            // P of the previous chunk (V phase -> M phase)
-  bf16x4 vf[2][2][2][2];                      // its V^T fragments [kb][st][db][lo / hi]
-  const int tr_key = 4 * half + ((lane & 15) >> 2);
-  const int tr_byte = ((lane >> 4) & 1) * 32 + (lane & 3) * 8;
-  const int swk = swz_kq(col), swv = swz_v(tr_key);
-  uint32_t va0[2];
-#pragma unroll
-  for (int db = 0; db < 2; ++db) {
-    const int byte = db * 64 + tr_byte;
-    va0[db] = KC * 128 + tr_key * 128 + (((byte >> 4) ^ swv) << 4) + (byte & 15);
-  }
-  int nkb_prev = 0;
-  for (int c = 0;; ++c) {
-    // ---------------- M(c)
-    const int kv0 = c * KC;
-    const int nkb = c < nch ? min(2, (N - kv0 + 31) >> 5) : 0;
-    if (active) {
-      bf16x8 kf[2][4];
-      const char* kl = smem + (c % NS) * SLOT;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-        if (kb < nkb) {
-#pragma unroll
-          for (int st = 0; st < 4; ++st)
-            kf[kb][st] = *reinterpret_cast<const bf16x8*>(kl + (kb * 32 + col) * 128 +
-                                                          (((st * 2 + half) ^ swk) << 4));
-        }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-        if (kb < nkb_prev) {
-#pragma unroll
-          for (int st = 0; st < 2; ++st) {
-#pragma unroll
-            for (int db = 0; db < 2; ++db) {
-              const bf16x4 lo = vf[kb][st][db][0], hi = vf[kb][st][db][1];
-              const bf16x8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-              o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb[kb][st], o[db], 0, 0, 0);
-            }
-            osum = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_ones, pb[kb][st], osum, 0, 0, 0);
-          }
-        }
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-        if (kb < nkb) {
-          s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_e0, b_m, zero, 0, 0, 0);   // -m_run
-#pragma unroll
-          for (int st = 0; st < 4; ++st)
-            s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][st], qf[st], s[kb], 0, 0, 0);
-        }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (grp == 1 && c + 1 < nch) vm_wait_n(2 * min(NS - 3, nch - 2 - c));   // chunk c + 1
-    __builtin_amdgcn_s_barrier();
-    if (c == nch) break;
-    // ---------------- V(c)
-    if (active) {
-      if (kv0 + KC > N) {                     // ragged last chunk: keys >= N are -inf
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = kv0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-            if (key >= N) s[kb][r] = -INFINITY;
-          }
-      }
-      float mx = -INFINITY;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-        if (kb < nkb) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
-        }
-      mx = pair_max(mx);
-      if (__builtin_amdgcn_ballot_w64(c == 0 || mx > 8.f)) {
-        const float m_new = bf16_round(m_run + (c == 0 ? mx : fmaxf(mx, 0.f)));
-        const float dlt = m_new - m_run;
-        const float alpha = c == 0 ? 0.f : __builtin_amdgcn_exp2f(-dlt);
-        m_run = m_new;
-        b_m[0] = (short)(half == 0 ? f32_to_bf16(-m_new) : 0);
-        osum[0] *= alpha;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) s[kb][r] -= dlt;
-      }
-      const uint32_t vs = lds_base + (c % NS) * SLOT;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-        if (kb < nkb) {
-#pragma unroll
-          for (int st = 0; st < 2; ++st)
-#pragma unroll
-            for (int db = 0; db < 2; ++db) {
-              const uint32_t a = vs + va0[db] + (kb * 32 + 16 * st) * 128;
-              asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(vf[kb][st][db][0]) : "v"(a));
-              asm volatile("ds_read_b64_tr_b16 %0, %1 offset:1024" : "=v"(vf[kb][st][db][1]) : "v"(a));
-            }
-#pragma unroll
-          for (int st = 0; st < 2; ++st) {
-            float e[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) e[j] = __builtin_amdgcn_exp2f(s[kb][8 * st + j]);
-            pb[kb][st] = __builtin_bit_cast(bf16x8, i32x4{(int)pack_bf16x2(e[0], e[1]),
-                                                          (int)pack_bf16x2(e[2], e[3]),
-                                                          (int)pack_bf16x2(e[4], e[5]),
-                                                          (int)pack_bf16x2(e[6], e[7])});
-          }
-        }
-    }
-    nkb_prev = nkb;
-    if (c + NS - 1 < nch) issue(c + NS - 1);
-    if (grp == 0 && c + 1 < nch) vm_wait_n(2 * min(NS - 2, nch - 2 - c));   // chunk c + 1
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // V(c) tr-reads retired: slot reuse
-    __builtin_amdgcn_s_barrier();
-  }
-  if (grp == 0) __builtin_amdgcn_s_barrier();   // equal barrier counts; the ring is free now
-  if (!active) return;
-  const float inv = 1.f / osum[0];
-  const int q = q0 + col;
-  if constexpr (MX8) {
-    if (q >= N) return;
-    uint8_t* qp = reinterpret_cast<uint8_t*>(out) + (row0 + q) * (int64_t)ldo + h * DKP;
-#pragma unroll
-    for (int db = 0; db < 2; ++db) {
-      float vv[16];
-      float amax = 0.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        vv[i] = bf16_round(o[db][i] * inv);
-        amax = fmaxf(amax, fabsf(vv[i]));
-      }
-      amax = pair_max(amax);
-      const int E = mx8_exponent(amax);
-      const float sinv = __uint_as_float((uint32_t)(127 - E) << 23);
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<uint32_t*>(qp + db * 32 + 8 * g + 4 * half) =
-            mx8_pack4(vv[4 * g], vv[4 * g + 1], vv[4 * g + 2], vv[4 * g + 3], sinv);
-      if (half == 0) {
-        const int k0 = h * DKP + db * 32;
-        s8[((int64_t)(k0 >> 7) * s_rows + row0 + q) * 4 + ((k0 >> 5) & 3)] = (uint8_t)(E + 127);
-      }
-    }
-    return;
-  } else {
-    // O restaged per wave (32 rows x 144 B, in the free ring) and stored as whole 128-B rows
-    char* wst = smem + wave * (32 * 144);
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<uint2*>(wst + col * 144 + (db * 32 + 8 * g + 4 * half) * 2) =
-            uint2{pack_bf16x2(o[db][4 * g + 0] * inv, o[db][4 * g + 1] * inv),
-                  pack_bf16x2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv)};
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int pass = 0; pass < 4; ++pass) {
-      const int r = pass * 8 + lrow;
-      if (q0 + r < N)
-        *reinterpret_cast<i32x4*>(out + (row0 + q0 + r) * ldo + h * DKP + lchunk * 8) =
-            *reinterpret_cast<const i32x4*>(wst + r * 144 + lchunk * 16);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------
 // Persistent short-sequence kernel, 16 queries per wave (bf16, DKP = 64, N in
 // (16 (NKB - 1), 16 NKB]; the C2 shape N = 196 is NKB = 13).  The 32-query kernel above runs
 // 2 waves per SIMD (7 active of 8 at N = 196) with ~190 registers each: its softmax chains
@@ -1925,31 +1658,6 @@ int launch_x3(const void* qkv, int B, int N, int heads, int ldqkv, float scale, 
   return VTD_OK;
 }
 
-// the ping-pong kernel for a bf16 attention of N keys (dkp 64): knob VTD_KNOB_ATTN_VARIANT 7
-bool pp_choice(int N) {
-  (void)N;
-  return knob(VTD_KNOB_ATTN_VARIANT) == 7;
-}
-
-template <bool MX8 = false>
-int launch_bf16_pp(const void* qkv, int B, int N, int heads, int ldqkv, float scale, void* out,
-                   int ldo, hipStream_t stream, uint8_t* s8 = nullptr, int64_t s_rows = 0) {
-  constexpr int LDS = 4 * 2 * 64 * 128;       // NS slots of K + V (>= the 8 x 32 x 144 B restage)
-  static std::once_flag once[kMaxDevices];
-  once_per_device(once, [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_bf16_pp_kernel<MX8>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-  });
-  const int nq = (N + 31) / 32, nqb = (nq + 7) / 8;
-  VTD_CHECK_ARG((int64_t)nqb * heads * B < INT32_MAX && (int64_t)N * ldqkv * 2 < INT32_MAX,
-                "attention: grid / image too large for the ping-pong kernel");
-  hipLaunchKernelGGL((attention_bf16_pp_kernel<MX8>), dim3(nqb * heads * B), dim3(512), LDS,
-                     stream, static_cast<const bf16_t*>(qkv), N, heads, ldqkv,
-                     scale * 1.4426950408889634f, static_cast<bf16_t*>(out), ldo, s8, s_rows, nqb);
-  VTD_LAUNCH_CHECK("attention_bf16_pp");
-  return VTD_OK;
-}
-
 template <int DKP, int NWG, bool MX8 = false>
 int launch_bf16_v2(const void* qkv, int B, int N, int heads, int ldqkv, float scale,
                    void* out, int ldo, hipStream_t stream, uint8_t* s8 = nullptr,
@@ -2040,9 +1748,6 @@ int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqk
     // streaming kernel at C3 / C5, profiles/r05_attn_fl_ab.log)
     if (dkp == 64 && ldqkv % 8 == 0 && ldo % 8 == 0 && v1 == 6)
       return launch_bf16_fl(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
-    // 7: the long-sequence ping-pong kernel (dkp 64)
-    if (dkp == 64 && pp_choice(N))
-      return launch_bf16_pp(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
     if (v1 == 1) {
       if (dkp == 32) return launch<bf16_t, 32>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
       if (dkp == 64) return launch<bf16_t, 64>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
@@ -2075,10 +1780,6 @@ int attention_mx8_launch(const void* qkv, int B, int N, int heads, int dkp, int 
   VTD_CHECK_ARG(s_rows >= (int64_t)B * N, "attention_mx8: s_rows < B * N");
   ProfScope ps(stream, PROF_ATTN,
                flops > 0 ? flops : 4.0 * B * heads * (double)N * N * dkp);
-  // the long-sequence ping-pong kernel where attention_launch (bf16) takes it, so that this
-  // equals vtd_attention + vtd_quantize_mx8 byte for byte under every knob setting
-  if (dkp == 64 && pp_choice(N))
-    return launch_bf16_pp<true>(qkv, B, N, heads, ldqkv, scale, q, ldq, stream, s, s_rows);
   if (dkp == 32)
     return launch_bf16_v2<32, 8, true>(qkv, B, N, heads, ldqkv, scale, q, ldq, stream, s, s_rows);
   if (dkp == 64)
