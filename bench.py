@@ -37,7 +37,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_TFLOPS = {"bf16": 2516.6, "f32": 157.3,    # MI355X dense: 256 CU x 2.4 GHz (MICROARCH)
-               "fp8": 5033.2}                    # block-scaled MX-fp8 MFMA: 2x bf16 per clock
+               "fp8": 5033.2,                    # block-scaled MX-fp8 MFMA: 2x bf16 per clock
+               "bf16x3": 2516.6}                 # split-bf16: bf16 MFMA (3 products per FLOP)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -412,7 +413,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256, help="images per GPU")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32", "fp8"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32", "fp8", "bf16x3"],
+                    help="bf16x3: the split-bf16 parity mode (the drop-in default dtype; "
+                         "roofline against the bf16 peak, FLOPs counted once although each is "
+                         "three bf16 MFMA products)")
     ap.add_argument("--preset", default="vit_b16_224")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--images", default="letterbox", choices=["letterbox", "uniform"],
@@ -451,7 +455,8 @@ def main():
     kw = dict(vtd.presets.PRESETS[args.preset])
     # identical weights on every rank (same seed): replicated-weight data parallelism
     model = vtd.create_vision_transformer_detector(
-        **kw, dtype={"bf16": "bfloat16", "f32": "float32", "fp8": "float8"}[args.dtype],
+        **kw, dtype={"bf16": "bfloat16", "f32": "float32", "fp8": "float8",
+                     "bf16x3": "bf16x3"}[args.dtype],
         device=dev, seed=0)
     kw = {k: model.kwargs[k] for k in model.kwargs}
     shape = model.input_shape

@@ -300,7 +300,11 @@ int ln_dispatch(const void* xv, int64_t rows, int D, int ldx, const float* g,
                    (reinterpret_cast<uintptr_t>(y) % (4 * sizeof(TO)) == 0) &&
                    (reinterpret_cast<uintptr_t>(g) % 16 == 0) &&
                    (reinterpret_cast<uintptr_t>(b) % 16 == 0);
-  if (vec && ln16_ok(xv, sizeof(TI) == 2 ? VTD_BF16 : VTD_F32, D, ldx, g, b)) {
+  // the 16-column kernel for the bf16 residual stream only: with an f32 stream (the f32 and
+  // split-bf16 parity modes) the 4-column kernel's fully coalesced 16-B loads win -- C2 B = 256
+  // per LayerNorm 105 -> 62 us (split-bf16 out, forward +1.8 %), 76 -> 49 us (f32 out, +1.6 %),
+  // profiles/r06_f32_stream_layernorm_ab.log
+  if (vec && sizeof(TI) == 2 && ln16_ok(xv, VTD_BF16, D, ldx, g, b)) {
     constexpr int RPW = 2;
     const dim3 g16((unsigned)((rows + 4 * RPW - 1) / (4 * RPW)));
     const int nc = (D + 1023) / 1024;
