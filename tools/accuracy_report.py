@@ -30,7 +30,7 @@ def main():
     dev = torch.device("cuda:0")
     res = {"resid_f32_env": os.environ.get("VTD_RESID_F32", "0")}
     seeded = json.load(open(os.path.join(GOLD, "seeded_forward.json")))
-    for dtype in ("float32", "bfloat16", "float8"):
+    for dtype in ("float32", "bf16x3", "bfloat16", "float8"):
         for name in ("tiny_mish", "tiny_gelu", "tiny_seq400"):
             z = np.load(os.path.join(GOLD, f"{name}.npz"))
             kw = json.loads(str(z["kwargs"]))

@@ -315,11 +315,16 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
   // score MFMA chain: one extra K-step multiplies the constant A column e_0 (1 at k = 0) by the
   // B column -m_run (k = 0), so each score leaves the matrix core as s - m_run and P is one
   // v_exp_f32 of it.  m_run starts at 0 and is set from the first chunk's max (`first`).
-  // SUMMFMA (dkp <= 64: register room): the row sum l rides in the PV MFMAs as a 32-row block
-  // of ones in V^T (every row of osum = sum_k P[k][q] of the bf16 P actually used), instead
-  // of one VALU add per score; otherwise l_run sums the fp32 P.
-  constexpr bool SUMMFMA = DKP <= 64;
-  float m_run = 0.f, l_run = 0.f;
+  // SUMMFMA: the row sum l rides in the PV MFMAs as a 32-row block of ones in V^T (every row
+  // of osum = sum_k P[k][q] of the bf16 P actually used), instead of one VALU add per score;
+  // otherwise l_run sums the fp32 P.  Both only where the registers allow it: the 4-wave
+  // workgroups (3 per CU; dkp <= 64 for SUMMFMA).  The 8-wave ones (C5's MX-fp8 epilogue,
+  // 2 workgroups per CU at <= 128 VGPRs) keep the running max outside the MFMA chain
+  // (OFFM false: P = exp2(s - m_run), m_run from -inf) -- with both tricks they took 141
+  // VGPRs, one workgroup per CU: C5 fp8 attention 261 -> 345 us (profiles/r06_s1_*).
+  constexpr bool OFFM = NWG == 4;
+  constexpr bool SUMMFMA = OFFM && DKP <= 64;
+  float m_run = OFFM ? 0.f : -INFINITY, l_run = 0.f;
   const bf16_t one_bf16 = 0x3F80;
   const bf16x8 a_e0 = {(short)(half == 0 ? one_bf16 : 0), 0, 0, 0, 0, 0, 0, 0};
   const bf16x8 a_ones = {(short)one_bf16, (short)one_bf16, (short)one_bf16, (short)one_bf16,
@@ -387,7 +392,8 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
       for (int kb = 0; kb < 2; ++kb) {
         if (kb < nkb) {
           const char* krow = kl + (kb * 32 + col) * C::KS;
-          s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_e0, b_m, zero, 0, 0, 0);   // -m_run
+          if constexpr (OFFM) s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_e0, b_m, zero, 0, 0, 0);   // -m_run
+          else s[kb] = zero;
 #pragma unroll
           for (int st = 0; st < C::KSTEPS; ++st)
             s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
@@ -417,30 +423,51 @@ __global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void
       // more than 8 (log2 units), so exp2 arguments stay <= 8 + 1/8 (P <= 2^8.125, exact in the
       // bf16 P operand's range, l and O in fp32); the final 1/l normalises whatever max was
       // used consistently for O and l.  The first chunk always sets the max.
-      if (__builtin_amdgcn_ballot_w64(c == 0 || mx > 8.f)) {
-        const float m_new = bf16_round(m_run + (c == 0 ? mx : fmaxf(mx, 0.f)));
-        const float dlt = m_new - m_run;
-        // (first chunk: O and l are still 0; dlt may be any size there)
-        const float alpha = c == 0 ? 0.f : __builtin_amdgcn_exp2f(-dlt);
-        m_run = m_new;
-        b_m[0] = (short)(half == 0 ? f32_to_bf16(-m_new) : 0);
-        l_run *= alpha;
-        osum[0] *= alpha;
+      if constexpr (OFFM) {
+        if (__builtin_amdgcn_ballot_w64(c == 0 || mx > 8.f)) {
+          const float m_new = bf16_round(m_run + (c == 0 ? mx : fmaxf(mx, 0.f)));
+          const float dlt = m_new - m_run;
+          // (first chunk: O and l are still 0; dlt may be any size there)
+          const float alpha = c == 0 ? 0.f : __builtin_amdgcn_exp2f(-dlt);
+          m_run = m_new;
+          b_m[0] = (short)(half == 0 ? f32_to_bf16(-m_new) : 0);
+          l_run *= alpha;
+          osum[0] *= alpha;
 #pragma unroll
-        for (int i = 0; i < C::DB; ++i)
+          for (int i = 0; i < C::DB; ++i)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+            for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[kb][r] -= dlt;
+        }
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
+          if (kb < nkb) {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) s[kb][r] -= dlt;
-      }
+            for (int r = 0; r < 16; ++r) s[kb][r] = __builtin_amdgcn_exp2f(s[kb][r]);
+          }
+      } else {
+        // (absolute scores) rescale only when some lane's max grows by more than 8
+        if (__builtin_amdgcn_ballot_w64(mx > m_run + 8.f)) {
+          const float m_new = fmaxf(m_run, mx);
+          const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+          m_run = m_new;
+          l_run *= alpha;
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-        if (kb < nkb) {
+          for (int i = 0; i < C::DB; ++i)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) s[kb][r] = __builtin_amdgcn_exp2f(s[kb][r]);
+            for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
         }
+        const float nm = -m_run;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+          if (kb < nkb) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[kb][r] = __builtin_amdgcn_exp2f(s[kb][r] + nm);
+          }
+      }
       if constexpr (!SUMMFMA) {
         // scalar fp32 adds (the file is built without SLP packing: packed f32 ops cost more
         // issue cycles beside MFMAs than two scalar ones); even / odd scores summed apart
@@ -1780,6 +1807,15 @@ int attention_mx8_launch(const void* qkv, int B, int N, int heads, int dkp, int 
   VTD_CHECK_ARG(s_rows >= (int64_t)B * N, "attention_mx8: s_rows < B * N");
   ProfScope ps(stream, PROF_ATTN,
                flops > 0 ? flops : 4.0 * B * heads * (double)N * N * dkp);
+  // the streaming kernel's workgroup size as attention_launch picks it under knob 2 (4 waves
+  // up to N = 128, else 8: C5's 576 keys), so that the two give the same bits
+  if (N <= 128) {
+    if (dkp == 32)
+      return launch_bf16_v2<32, 4, true>(qkv, B, N, heads, ldqkv, scale, q, ldq, stream, s, s_rows);
+    if (dkp == 64)
+      return launch_bf16_v2<64, 4, true>(qkv, B, N, heads, ldqkv, scale, q, ldq, stream, s, s_rows);
+    return launch_bf16_v2<128, 4, true>(qkv, B, N, heads, ldqkv, scale, q, ldq, stream, s, s_rows);
+  }
   if (dkp == 32)
     return launch_bf16_v2<32, 8, true>(qkv, B, N, heads, ldqkv, scale, q, ldq, stream, s, s_rows);
   if (dkp == 64)
