@@ -1396,219 +1396,6 @@ int launch_bf16_fl(const void* qkv, int B, int N, int heads, int ldqkv, float sc
 }
 
 // ---------------------------------------------------------------------------------
-// Streaming kernel, 16 queries per wave (bf16, DKP = 64; knob VTD_KNOB_ATTN_VARIANT 8).
-// attention_bf16_kernel's register-staged 64-key chunks and deferred-rescale online softmax
-// on v_mfma_f32_16x16x32_bf16: a wave holds 16 queries, so its score tile is 4 blocks of 16
-// keys x 16 queries (4 registers each) and its O^T 4 blocks of 16 d (16 registers): about half
-// the registers of the 32-query kernel at the same VALU per score.
-//   S^T block kb = K[16 kb .. +15] . Q^T: lane l holds query q0 + (l & 15) and keys
-//   16 kb + 4 g + r (g = l >> 4, r = 0..3);
-//   O^T += V^T . P^T per 32-key step: P^T's 8 K-elements of lane l are its own scores of the
-//   step's two blocks (keys 32 s + 4 g + 0..3 and 32 s + 16 + 4 g + 0..3), V^T's the same keys
-//   by two ds_read_b64_tr_b16 (one 4-key x 16-d block per 16-lane group); the row sum as a
-//   block of ones in V^T (osum).  Row max over the query's four lanes (l, l ^ 16, l ^ 32,
-//   l ^ 48): in-lane, then the gfx950 lane swaps.
-// LDS rows: K 144 B (the 16 rows of a ds_read_b128 lane group cover 64 banks once), V 160 B
-// (the 8 rows x 32 B of a tr-read half-wave cover 64 banks once).
-__device__ __forceinline__ float max_lane16(float v) {
-  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false,
-                                                  false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
-template <int NW>
-__global__ __launch_bounds__(64 * NW, 2) void attention_bf16_s16_kernel(
-    const bf16_t* __restrict__ qkv, int N, int heads, int ldqkv, float scale_log2,
-    bf16_t* __restrict__ out, int ldo, int nqb) {
-  constexpr int DKP = 64, KC = 64, KS = 144, VS = 160;
-  constexpr int BUF = KC * KS + KC * VS;
-  constexpr int CPR = DKP * 2 / 16, NCH = KC * CPR * 2;
-  constexpr int nthreads = 64 * NW;
-  constexpr int NPASS = (NCH + nthreads - 1) / nthreads;
-  typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6, g = lane >> 4, fr = lane & 15;
-  int v = blockIdx.x;                         // XCD-aware: a pair's query blocks share an XCD
-  {
-    const int G = gridDim.x, xcd = v & 7, q8 = G >> 3, r8 = G & 7;
-    v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (v >> 3);
-  }
-  const int pair = v / nqb, qb = v - pair * nqb;
-  const int b = pair / heads, h = pair - b * heads;
-  const int inner = heads * DKP;
-  const int64_t row0 = (int64_t)b * N;
-  const int q0 = (qb * NW + wave) * 16;
-  const bool active = q0 < N;
-
-  bf16x8 qf[2];                               // pre-scaled to log2 units (attention_bf16_kernel)
-  {
-    const int q = min(q0 + fr, N - 1);
-    const bf16_t* qp = qkv + (row0 + q) * ldqkv + h * DKP;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const i32x4 raw = *reinterpret_cast<const i32x4*>(qp + 32 * ks + 8 * g);
-      i32x4 sc;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        sc[j] = (int)pack_bf16x2(__uint_as_float((uint32_t)raw[j] << 16) * scale_log2,
-                                 __uint_as_float((uint32_t)raw[j] & 0xffff0000u) * scale_log2);
-      qf[ks] = __builtin_bit_cast(bf16x8, sc);
-    }
-  }
-  f32x4 o[4], osum = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int db = 0; db < 4; ++db) o[db] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run = -INFINITY;
-  const bf16_t one_bf16 = 0x3F80;
-  const bf16x8 a_ones = {(short)one_bf16, (short)one_bf16, (short)one_bf16, (short)one_bf16,
-                         (short)one_bf16, (short)one_bf16, (short)one_bf16, (short)one_bf16};
-
-  i32x4 stg[NPASS];
-  auto gload = [&](int kv0) {
-#pragma unroll
-    for (int i = 0; i < NPASS; ++i) {
-      const int c = tid + i * nthreads;
-      if (c < NCH) {
-        const int isv = c >= KC * CPR;
-        const int cc = c - isv * KC * CPR;
-        const int kr = cc / CPR, ch = cc - kr * CPR;
-        const int key = min(kv0 + kr, N - 1);
-        stg[i] = *reinterpret_cast<const i32x4*>(qkv + (row0 + key) * ldqkv + (1 + isv) * inner +
-                                                 h * DKP + ch * 8);
-      }
-    }
-  };
-  auto swrite = [&](int buf) {
-    char* base = smem + buf * BUF;
-#pragma unroll
-    for (int i = 0; i < NPASS; ++i) {
-      const int c = tid + i * nthreads;
-      if (c < NCH) {
-        const int isv = c >= KC * CPR;
-        const int cc = c - isv * KC * CPR;
-        const int kr = cc / CPR, ch = cc - kr * CPR;
-        char* dst = isv ? base + KC * KS + kr * VS + ch * 16 : base + kr * KS + ch * 16;
-        *reinterpret_cast<i32x4*>(dst) = stg[i];
-      }
-    }
-  };
-  const int nchunks = (N + KC - 1) / KC;
-  gload(0);
-  swrite(0);
-  __syncthreads();
-  // tr-read: lane 4 q + p of a 16-lane group addresses key row q of the 4-key block, d 4 p
-  const int tr_off = (4 * g + (fr >> 2)) * VS + (fr & 3) * 8;
-  auto chunk = [&](int c, auto last_tag) {
-    constexpr bool LAST = decltype(last_tag)::value;
-    const int kv0 = c * KC;
-    if (!LAST) gload(kv0 + KC);
-    if (active) {
-      const char* kl = smem + (c & 1) * BUF;
-      const char* vl = kl + KC * KS;
-      const int nkb = LAST ? min(4, (N - kv0 + 15) >> 4) : 4;   // 16-key blocks with a key
-      f32x4 s[4];
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb) {
-        if (kb < nkb) {
-          const char* krow = kl + (16 * kb + fr) * KS + 16 * g;
-          s[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(krow),
-                                                          qf[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          s[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              *reinterpret_cast<const bf16x8*>(krow + 64), qf[1], s[kb], 0, 0, 0);
-        } else {
-          s[kb] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-        }
-      }
-      if (LAST && kv0 + KC > N) {             // keys >= N
-#pragma unroll
-        for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (kv0 + 16 * kb + 4 * g + r >= N) s[kb][r] = -INFINITY;
-      }
-      float mx = -INFINITY;
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
-        mx = fmaxf(mx, fmaxf(fmaxf(s[kb][0], s[kb][1]), fmaxf(s[kb][2], s[kb][3])));
-      mx = max_lane16(pair_max(mx));
-      if (__builtin_amdgcn_ballot_w64(mx > m_run + 8.f)) {
-        const float m_new = fmaxf(m_run, mx);
-        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-        m_run = m_new;
-        osum *= alpha;
-#pragma unroll
-        for (int db = 0; db < 4; ++db) o[db] *= alpha;
-      }
-      const float nm = -m_run;
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        if (2 * st < nkb) {
-          float e[8];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            e[j] = __builtin_amdgcn_exp2f(s[2 * st][j] + nm);
-            e[4 + j] = __builtin_amdgcn_exp2f(s[2 * st + 1][j] + nm);   // -inf past N: 0
-          }
-          const bf16x8 pb = __builtin_bit_cast(bf16x8, i32x4{(int)pack_bf16x2(e[0], e[1]),
-                                                             (int)pack_bf16x2(e[2], e[3]),
-                                                             (int)pack_bf16x2(e[4], e[5]),
-                                                             (int)pack_bf16x2(e[6], e[7])});
-          const char* va = vl + 32 * st * VS + tr_off;
-#pragma unroll
-          for (int db = 0; db < 4; ++db) {
-            const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(va + 32 * db));
-            const bf16x4 hi =
-                __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(va + 16 * VS + 32 * db));
-            const bf16x8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            o[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, pb, o[db], 0, 0, 0);
-          }
-          osum = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_ones, pb, osum, 0, 0, 0);
-        }
-      }
-    }
-    if (!LAST) swrite((c + 1) & 1);
-    __syncthreads();
-  };
-  for (int c = 0; c + 1 < nchunks; ++c) chunk(c, std::false_type{});
-  chunk(nchunks - 1, std::true_type{});
-  if (!active) return;
-  const float inv = 1.f / osum[0];
-  // O restaged per wave (16 query rows x 144 B, in the LDS free after the last barrier), then
-  // whole 128-B rows
-  char* wst = smem + wave * (16 * 144);
-#pragma unroll
-  for (int db = 0; db < 4; ++db)
-    *reinterpret_cast<uint2*>(wst + fr * 144 + 32 * db + 8 * g) =
-        uint2{pack_bf16x2(o[db][0] * inv, o[db][1] * inv), pack_bf16x2(o[db][2] * inv, o[db][3] * inv)};
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // wave-local: own writes landed
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    const int r = pass * 8 + (lane >> 3), ch = lane & 7;
-    if (q0 + r < N)
-      *reinterpret_cast<i32x4*>(out + (row0 + q0 + r) * ldo + h * DKP + ch * 8) =
-          *reinterpret_cast<const i32x4*>(wst + r * 144 + ch * 16);
-  }
-}
-
-template <int NW>
-int launch_bf16_s16(const void* qkv, int B, int N, int heads, int ldqkv, float scale, void* out,
-                    int ldo, hipStream_t stream) {
-  constexpr int LDS = 2 * 64 * (144 + 160);
-  const int nq = (N + 15) / 16, nqb = (nq + NW - 1) / NW;
-  VTD_CHECK_ARG((int64_t)nqb * heads * B < INT32_MAX, "attention: grid too large");
-  static std::once_flag once[kMaxDevices];
-  once_per_device(once, [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_bf16_s16_kernel<NW>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-  });
-  hipLaunchKernelGGL((attention_bf16_s16_kernel<NW>), dim3(nqb * heads * B), dim3(64 * NW), LDS,
-                     stream, static_cast<const bf16_t*>(qkv), N, heads, ldqkv,
-                     scale * 1.4426950408889634f, static_cast<bf16_t*>(out), ldo, nqb);
-  VTD_LAUNCH_CHECK("attention_bf16_s16");
-  return VTD_OK;
-}
-
-// ---------------------------------------------------------------------------------
 // Split-bf16 kernel (the VTD_BF16X3 parity mode; include/vtd.h "Split-bf16 operands").
 // Q, K, V arrive as f32 (the query/key/value GEMM's f32 output) and every product runs on
 // the bf16 MFMA as three: hi.hi + lo.hi + hi.lo with hi = bf16(v), lo = bf16(v - hi), fp32
@@ -1988,9 +1775,6 @@ int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqk
     // streaming kernel at C3 / C5, profiles/r05_attn_fl_ab.log)
     if (dkp == 64 && ldqkv % 8 == 0 && ldo % 8 == 0 && v1 == 6)
       return launch_bf16_fl(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
-    // 8 / 9: the 16-query streaming kernel, 8 / 4 waves per workgroup (dkp 64)
-    if (dkp == 64 && v1 == 8) return launch_bf16_s16<8>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
-    if (dkp == 64 && v1 == 9) return launch_bf16_s16<4>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
     if (v1 == 1) {
       if (dkp == 32) return launch<bf16_t, 32>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
       if (dkp == 64) return launch<bf16_t, 64>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
