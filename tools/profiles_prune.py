@@ -13,7 +13,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF = os.path.join(ROOT, "profiles")
 DOCS = ["DESIGN.md", "BASELINE.md", "README.md", "INTEGRATION.md", "bench.py"]
-TOK = re.compile(r"(?:profiles/)?((?:r\d\d|gemm)_[A-Za-z0-9_.{},\-]*[A-Za-z0-9}])")
+TOK = re.compile(r"(?:profiles/)?((?:r\d\d|gemm)_[A-Za-z0-9_.{},*\-]*[A-Za-z0-9}*])")
 
 
 def expand(tok):
@@ -37,10 +37,12 @@ def cited():
 
 def main():
     dry = "--dry-run" in sys.argv
+    import fnmatch
     keep = cited()
+    pats = [n for n in keep if "*" in n]                    # `r06_s2_*`: every file it matches
     files = sorted(f for f in os.listdir(PROF) if os.path.isfile(os.path.join(PROF, f)))
-    moved = [f for f in files if f not in keep]
-    missing = sorted(n for n in keep if "." in n and not os.path.exists(os.path.join(PROF, n))
+    moved = [f for f in files if f not in keep and not any(fnmatch.fnmatch(f, p) for p in pats)]
+    missing = sorted(n for n in keep if "." in n and "*" not in n and not os.path.exists(os.path.join(PROF, n))
                      and not os.path.exists(os.path.join(ROOT, n)))
     print(f"{len(files)} files, {len(files) - len(moved)} cited, {len(moved)} to archive/")
     for n in missing:
