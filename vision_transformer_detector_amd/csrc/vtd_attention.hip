@@ -1780,7 +1780,10 @@ int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqk
       if (dkp == 64) return launch<bf16_t, 64>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
       return launch<bf16_t, 128>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
     }
-    if (v1 == 3 || (v1 == 2 && N > 128)) {   // 8-wave workgroups (one (b,h) per WG to N=256)
+    // 8-wave workgroups (one (b,h) per WG to N=256): knob 3 always, knob 2 from N = 129, and the
+    // default (4) for dkp 64 from N = 257 (C3 / C5: 311-330 vs 339-397 us at C3, 255-257 vs
+    // 270-284 us at C5; 2 workgroups per CU at <= 128 VGPRs, profiles/r06_attn_8wave_default_ab.log)
+    if (v1 == 3 || (v1 == 2 && N > 128) || (v1 == 4 && dkp == 64 && N > 256)) {
       if (dkp == 32) return launch_bf16_v2<32, 8>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
       if (dkp == 64) return launch_bf16_v2<64, 8>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
       return launch_bf16_v2<128, 8>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
