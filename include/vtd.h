@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define VTD_ABI_VERSION 15
+#define VTD_ABI_VERSION 16
 #define VTD_KALIGN 64          /* K / row padding granule, elements              */
 #define VTD_MAX_MLP 16         /* max encoder_mlp_quantities                     */
 #define VTD_MAX_HEAD 64        /* max mlp_head layers * repeats                   */
@@ -56,14 +56,15 @@ typedef enum vtd_dtype {       /* compute (GEMM operand) dtype                  
 /* Split-bf16 operands (VTD_BF16X3).  An f32 value v is held as hi = bf16(v) (round to
  * nearest even) and lo = bf16(v - hi): hi + lo carries 16 significand bits, and
  * hi_a hi_b + lo_a hi_b + hi_a lo_b leaves out only lo_a lo_b (<= 2^-18 |a b|).  A K-wide
- * f32 row is stored as a bf16 row of THREE P-wide pieces (P = row stride / 3 >= K, the
+ * f32 row is stored as a bf16 row of P-wide pieces (P >= K, P % 64 == 0 for a GEMM, the
  * columns [K, P) of every piece zero):
- *   A operand (activations, role 0):  [ hi | lo | hi ]
- *   B operand (weights W^T, role 1):  [ hi | hi | lo ]
- * so one ordinary bf16 GEMM over K' = 3 P (vtd_gemm, dtype VTD_BF16, lda = ldb = 3 P) sums
- * the three products in its fp32 accumulators.  Producers write the A form directly:
- * vtd_epilogue.out_dtype = VTD_BF16X3, vtd_layernorm / vtd_extract_patches with
- * dtype = VTD_BF16X3 (ldo / ldy = 3 P); vtd_split_bf16x3 converts any f32 matrix. */
+ *   A operand (activations, role 0):  [ hi | lo ]        (row stride >= 2 P)
+ *   B operand (weights W^T, role 1):  [ hi | hi | lo ]   (row stride >= 3 P)
+ * and vtd_gemm with dtype VTD_BF16X3, K = 3 P, reads each A row as [hi | lo | hi] (its K loop
+ * returns to A's column 0 after 2 P) against the B row: one bf16 GEMM whose fp32
+ * accumulators sum the three products.  Producers write the A form directly:
+ * vtd_epilogue.out_dtype = VTD_BF16X3, vtd_layernorm / vtd_extract_patches / vtd_attention
+ * with dtype = VTD_BF16X3 (ldo / ldy = 2 P); vtd_split_bf16x3 converts any f32 matrix. */
 
 typedef enum vtd_act {         /* activation fused in a GEMM epilogue            */
   VTD_ACT_NONE = 0,
@@ -164,9 +165,9 @@ int vtd_pack_dense(const float* src_dev, int K, int N, int k_group, int k_group_
 int vtd_pack_vector(const float* src_dev, int N, int n_group, int n_group_p,
                     float* dst_dev, int offset, void* stream);
 
-/* f32 x [rows][ldx] (first K columns) -> split-bf16 y [rows][ldy] (three P = ldy / 3 wide
- * pieces, P >= K; role 0: [hi | lo | hi], role 1: [hi | hi | lo]; columns [K, P) of each
- * piece written as zero).  ldy % 3 == 0. */
+/* f32 x [rows][ldx] (first K columns) -> split-bf16 y [rows][ldy], P >= K wide pieces
+ * (columns [K, P) of each piece written as zero): role 0 the A operand [hi | lo], P = ldy / 2
+ * (ldy % 2 == 0); role 1 the B operand [hi | hi | lo], P = ldy / 3 (ldy % 3 == 0). */
 int vtd_split_bf16x3(const float* x_dev, int64_t rows, int K, int ldx, void* y_dev, int ldy,
                      int role, void* stream);
 
@@ -174,7 +175,7 @@ int vtd_split_bf16x3(const float* x_dev, int64_t rows, int K, int ldx, void* y_d
 /* ExtractImagePatches (vtd.py:177-206) + Reshape flatten_patches (vtd.py:279-280):
  * images NHWC fp32 [B][H][W][C] -> patches [B*N][ld_out] (dtype), SAME zero pad,
  * (kh, kw, c) order; columns [P, ld_out) written as zero.  dtype VTD_BF16X3: the split-bf16
- * A operand, three ld_out / 3 wide pieces. */
+ * A operand, two ld_out / 2 wide pieces (ld_out % 16 == 0). */
 int vtd_extract_patches(const float* images_dev, int B, int H, int W, int C, int p,
                         void* out_dev, int ld_out, int dtype, void* stream);
 
@@ -182,9 +183,11 @@ int vtd_extract_patches(const float* images_dev, int B, int H, int W, int C, int
  * C[m][n] = act(sum_k A[m][k] * Bt[n][k] + bias[n] + rowadd[m % rowadd_period]
  *               (rowadd only for n < rowadd_ncols)) + resid[m][n]
  * for m < M, n < N.  A, Bt in `dtype`; K % VTD_KALIGN == 0; lda, ldb % 8 == 0.
+ * dtype VTD_BF16X3: bf16 operands, A the split-bf16 A operand [hi | lo] (lda >= 2 K / 3), Bt
+ * the B operand (ldb >= K), K = 3 P with P % 64 == 0 (see "Split-bf16 operands").
  * out: fp32 (out_dtype 0), bf16 (1) or split-bf16 (VTD_BF16X3: the next GEMM's A operand
- * [hi | lo | hi], three ldo / 3 wide pieces, ldo % 3 == 0, ldo / 3 >= N; dtype VTD_BF16
- * only); out2 (nullable) a second bf16 copy.
+ * [hi | lo], two ldo / 2 wide pieces, ldo % 2 == 0, ldo / 2 >= N; bf16 / split-bf16
+ * operands only); out2 (nullable) a second bf16 copy.
  * scatter_tokens > 0 selects the head Reshape epilogue (vtd.py:461-463): element
  * (m = b*T + t, n < 17) is stored at out[(b*17 + f / T) * ldo + f % T], f = t*17 + n. */
 typedef struct vtd_epilogue {
@@ -221,16 +224,17 @@ typedef struct vtd_epilogue {
 } vtd_epilogue;
 int vtd_gemm(int M, int N, int K, const void* A_dev, int lda, const void* Bt_dev,
              int ldb, int dtype, const vtd_epilogue* epi, void* stream);
-/* Split-K form of vtd_gemm (bf16 only; what vtd_forward runs for the detection head's
- * few-tile, long-K Dense layers, vtd.py:468-486): `ksplit` K ranges of K / 64 / ksplit
+/* Split-K form of vtd_gemm (dtype VTD_BF16 or VTD_BF16X3; what vtd_forward runs for the
+ * detection head's few-tile, long-K Dense layers, vtd.py:468-486): `ksplit` K ranges of
+ * K / 64 / ksplit
  * K-steps each write fp32 partial sums into part_dev ([ksplit][M][N] floats,
  * part_bytes >= ksplit * M * N * 4), then one pass sums them in split order and applies
  * the epilogue (no LayerNorm fold / statistics).  K % 64 == 0, N % 4 == 0,
  * 2 <= ksplit <= K / 64 with every split non-empty.  vtd_gemm_splitk_choice returns the
  * split count vtd_forward uses for (M, N, K, dtype) (1 = no split). */
 int vtd_gemm_splitk(int M, int N, int K, const void* A_dev, int lda, const void* Bt_dev,
-                    int ldb, const vtd_epilogue* epi, float* part_dev, size_t part_bytes,
-                    int ksplit, void* stream);
+                    int ldb, int dtype, const vtd_epilogue* epi, float* part_dev,
+                    size_t part_bytes, int ksplit, void* stream);
 int vtd_gemm_splitk_choice(int M, int N, int K, int dtype);
 
 /* MX-fp8 operands (OCP MX: e4m3 elements, one E8M0 scale byte e = 2^(e-127) per 32
@@ -256,7 +260,7 @@ int vtd_gemm_mx8(int M, int N, int K, const uint8_t* A_dev, int lda, const uint8
 /* keras LayerNormalization(axis=-1, epsilon) (vtd.py:353-357, 375-379):
  * x (x_dtype: fp32, or the bf16 residual stream) [rows][ldx] -> y (dtype) [rows][ldy];
  * fp32 statistics over the first D columns; columns [D, ldy) of y written as zero.
- * dtype VTD_BF16X3: y is the split-bf16 A operand, three ldy / 3 wide pieces. */
+ * dtype VTD_BF16X3: y is the split-bf16 A operand, two ldy / 2 wide pieces. */
 int vtd_layernorm(const void* x_dev, int x_dtype, int64_t rows, int D, int ldx,
                   const float* gamma_dev, const float* beta_dev, float eps,
                   void* y_dev, int ldy, int dtype, void* stream);
@@ -290,8 +294,8 @@ int vtd_fold_layernorm(const float* w32_dev, int N, int K, int ldw, const float*
  * out [B*N][ldo] at column h*dkp.  dkp in {32, 64, 128}; scale = 1/sqrt(key_dim).
  * dtype VTD_BF16X3 (the split-bf16 parity mode): qkv is fp32, every product runs as three
  * bf16 MFMA products (hi.hi + lo.hi + hi.lo, fp32 softmax statistics), and out is the
- * split-bf16 A operand of the attention-output Dense, [hi | lo | hi] in three ldo / 3 wide
- * pieces (ldo % 3 == 0, ldo / 3 >= heads*dkp; columns [heads*dkp, ldo / 3) not written). */
+ * split-bf16 A operand of the attention-output Dense, [hi | lo] in two ldo / 2 wide pieces
+ * (ldo % 2 == 0, ldo / 2 >= heads*dkp; columns [heads*dkp, ldo / 2) not written). */
 int vtd_attention(const void* qkv_dev, int B, int N, int heads, int dkp, int ldqkv,
                   float scale, void* out_dev, int ldo, int dtype, void* stream);
 

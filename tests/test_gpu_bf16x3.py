@@ -1,8 +1,9 @@
 """Split-bf16 parity mode (dtype VTD_BF16X3 / "bf16x3"; include/vtd.h "Split-bf16 operands").
 
 An f32 value v is held as hi = bf16(v) (round to nearest even) and lo = bf16(v - hi); a Dense
-layer runs as ONE bf16 MFMA GEMM over K' = 3 K on the rows [hi | lo | hi] (activations, A) and
-[hi | hi | lo] (weights, B), i.e. hi.hi + lo.hi + hi.lo summed in fp32 accumulators.  Checks:
+layer runs as ONE bf16 MFMA GEMM over K' = 3 K on the activation rows stored [hi | lo] and read
+as [hi | lo | hi] (A: the K loop returns to column 0 after 2 K) against the weight rows
+[hi | hi | lo] (B), i.e. hi.hi + lo.hi + hi.lo summed in fp32 accumulators.  Checks:
   * the split itself is bit-exact against a numpy restatement (split_np below);
   * every producer that writes the split operand directly -- the GEMM epilogues (generic,
     LDS-staged fast, register-direct transposed; the head's Reshape scatter; split-K), the
@@ -40,14 +41,14 @@ def bf16_to_f32(b):
 
 
 def split_np(x, P, role):
-    """f32 [rows][K] -> uint16 [rows][3P]: role 0 [hi | lo | hi], role 1 [hi | hi | lo]."""
+    """f32 [rows][K] -> uint16: role 0 [hi | lo] ([rows][2P]), role 1 [hi | hi | lo] ([rows][3P])."""
     x = np.asarray(x, np.float32)
     rows, K = x.shape
     xp = np.zeros((rows, P), np.float32)
     xp[:, :K] = x
     hi = bf16_rne(xp)
     lo = bf16_rne(xp - bf16_to_f32(hi))
-    return np.concatenate([hi, lo, hi] if role == 0 else [hi, hi, lo], axis=1)
+    return np.concatenate([hi, lo] if role == 0 else [hi, hi, lo], axis=1)
 
 
 def as_u16(t):
@@ -56,8 +57,9 @@ def as_u16(t):
 
 def split_dev(L, x, P, role):
     rows, K = x.shape
-    y = torch.full((rows, 3 * P), -1, dtype=torch.int16, device=x.device)
-    L.check(L.lib.vtd_split_bf16x3(x.data_ptr(), rows, K, x.shape[1], y.data_ptr(), 3 * P, role,
+    w = (3 if role else 2) * P
+    y = torch.full((rows, w), -1, dtype=torch.int16, device=x.device)
+    L.check(L.lib.vtd_split_bf16x3(x.data_ptr(), rows, K, x.shape[1], y.data_ptr(), w, role,
                                    L.stream_ptr()), "split")
     torch.cuda.synchronize()
     return y.view(torch.bfloat16)
@@ -92,23 +94,38 @@ def _gemm_x3(L, A32, W32, N=None, **kw):
 
 
 @pytest.mark.parametrize("M,N,K", [(64, 64, 64), (300, 200, 192), (1024, 768, 768),
-                                   (8192, 1024, 256), (512, 17, 256)])
+                                   (8192, 1024, 256), (512, 17, 256), (300, 512, 192),
+                                   (2048, 2048, 3072), (2176, 2176, 1088)])
 def test_split_gemm_vs_fp64(L, cuda, M, N, K):
-    """A split-bf16 GEMM (bf16 kernels over K' = 3K: the 256-tile pp2 kernel for the larger
-    shapes, the 128-tile / skinny kernels for the small ones) against the fp64 product of the
-    f32 operands."""
+    """A split-bf16 GEMM (dtype VTD_BF16X3: bf16 kernels over K' = 3K, A read with the wrap --
+    the 256-tile pp2 kernel for the larger shapes, the 128-tile kernel (1024 x 768, 300 x 512)
+    and the skinny kernel for the small ones) against the fp64 product of the f32 operands;
+    where the forward would split K (vtd_gemm_splitk_choice), the split-K form too, whose
+    ranges start before, across and past the wrap (2176 x 2176 x 1088: 4 x 13 K-steps, wrap
+    at 34)."""
     g = torch.Generator().manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g)
     W = torch.randn(N, K, generator=g) / math.sqrt(K)
     a3, b3 = _gemm_x3(L, A.to(cuda), W.to(cuda))
+    ref64 = A.double() @ W.double().T
     out = torch.full((M, N), float("nan"), device=cuda)
     e = _epi(L, out, N, L.F32)
-    L.check(L.lib.vtd_gemm(M, N, 3 * K, a3.data_ptr(), 3 * K, b3.data_ptr(), 3 * K, L.BF16,
+    L.check(L.lib.vtd_gemm(M, N, 3 * K, a3.data_ptr(), 2 * K, b3.data_ptr(), 3 * K, L.BF16X3,
                            ctypes.byref(e), L.stream_ptr()), "gemm")
+    ks = L.lib.vtd_gemm_splitk_choice(M, N, 3 * K, L.BF16X3)
+    outs = [out]
+    if ks > 1:
+        out2 = torch.full((M, N), float("nan"), device=cuda)
+        e2 = _epi(L, out2, N, L.F32)
+        part = torch.empty(ks * M * N, device=cuda)
+        L.check(L.lib.vtd_gemm_splitk(M, N, 3 * K, a3.data_ptr(), 2 * K, b3.data_ptr(), 3 * K,
+                                      L.BF16X3, ctypes.byref(e2), part.data_ptr(),
+                                      part.numel() * 4, ks, L.stream_ptr()), "splitk")
+        outs.append(out2)
     torch.cuda.synchronize()
-    ref64 = A.double() @ W.double().T
-    err = (out.cpu().double() - ref64).abs().max().item()
-    assert err <= 2e-5 * ref64.abs().max().item(), err
+    for o in outs:
+        err = (o.cpu().double() - ref64).abs().max().item()
+        assert err <= 2e-5 * ref64.abs().max().item(), (len(outs), err)
 
 
 @pytest.mark.parametrize("M,N,K,act", [(8192, 1024, 256, 0), (4096, 3072, 256, 1),
@@ -125,13 +142,13 @@ def test_split_output_equals_split_of_f32_output(L, cuda, M, N, K, act):
     bias = torch.randn(N, generator=g).to(cuda)
     f32 = torch.empty(M, N, device=cuda)
     P = ((N + 63) // 64) * 64
-    s3 = torch.full((M, 3 * P), -1, dtype=torch.int16, device=cuda)
-    for out, ldo, od in ((f32, N, L.F32), (s3, 3 * P, L.BF16X3)):
+    s3 = torch.full((M, 2 * P), -1, dtype=torch.int16, device=cuda)
+    for out, ldo, od in ((f32, N, L.F32), (s3, 2 * P, L.BF16X3)):
         e = _epi(L, out, ldo, od, bias=bias, act=act)
         ks = L.lib.vtd_gemm_splitk_choice(M, N, K, L.BF16)
         if ks > 1:
             part = torch.empty(ks * M * N, device=cuda)
-            L.check(L.lib.vtd_gemm_splitk(M, N, K, A.data_ptr(), K, W.data_ptr(), K,
+            L.check(L.lib.vtd_gemm_splitk(M, N, K, A.data_ptr(), K, W.data_ptr(), K, L.BF16,
                                           ctypes.byref(e), part.data_ptr(), part.numel() * 4, ks,
                                           L.stream_ptr()), "splitk")
         else:
@@ -141,8 +158,9 @@ def test_split_output_equals_split_of_f32_output(L, cuda, M, N, K, act):
     v = f32.cpu().numpy()
     want = split_np(v, P, 0)
     got = as_u16(s3)
-    # columns [N, P) of each piece are not written; the third piece repeats the first
-    assert np.array_equal(got[:, 2 * P:2 * P + N], got[:, :N])
+    # columns [N, P) of each piece are not written
+    if N < P:
+        assert (got[:, N:P] == 0xFFFF).all() and (got[:, P + N:] == 0xFFFF).all()
     if act == 0:
         for piece in range(2):
             sl = slice(piece * P, piece * P + N)
@@ -166,8 +184,8 @@ def test_split_scatter_epilogue(L, cuda):
     bias = torch.randn(17, generator=g).to(cuda)
     P = 256
     f32 = torch.zeros(B * 17, P, device=cuda)
-    s3 = torch.zeros(B * 17, 3 * P, dtype=torch.int16, device=cuda)
-    for out, ldo, od in ((f32, P, L.F32), (s3, 3 * P, L.BF16X3)):
+    s3 = torch.zeros(B * 17, 2 * P, dtype=torch.int16, device=cuda)
+    for out, ldo, od in ((f32, P, L.F32), (s3, 2 * P, L.BF16X3)):
         e = _epi(L, out, ldo, od, bias=bias, scatter=T)
         L.check(L.lib.vtd_gemm(B * T, 17, K, A.data_ptr(), K, W.data_ptr(), K, L.BF16,
                                ctypes.byref(e), L.stream_ptr()), "gemm")
@@ -189,8 +207,8 @@ def test_layernorm_split_output(L, cuda, rows, D, P, xdt):
     gamma = (1 + 0.1 * torch.randn(P, generator=g)).to(cuda)
     beta = (0.1 * torch.randn(P, generator=g)).to(cuda)
     f32 = torch.empty(rows, P, device=cuda)
-    s3 = torch.full((rows, 3 * P), -1, dtype=torch.int16, device=cuda)
-    for out, ldy, od in ((f32, P, L.F32), (s3, 3 * P, L.BF16X3)):
+    s3 = torch.full((rows, 2 * P), -1, dtype=torch.int16, device=cuda)
+    for out, ldy, od in ((f32, P, L.F32), (s3, 2 * P, L.BF16X3)):
         L.check(L.lib.vtd_layernorm(x.data_ptr(), code, rows, D, P, gamma.data_ptr(),
                                     beta.data_ptr(), 1e-3, out.data_ptr(), ldy, od,
                                     L.stream_ptr()), "layernorm")
@@ -205,8 +223,8 @@ def test_patches_split_output(L, cuda, H, W, p, P):
     gh, gw = -(-H // p), -(-W // p)
     rows = 2 * gh * gw
     f32 = torch.empty(rows, P, device=cuda)
-    s3 = torch.full((rows, 3 * P), -1, dtype=torch.int16, device=cuda)
-    for out, ldo, od in ((f32, P, L.F32), (s3, 3 * P, L.BF16X3)):
+    s3 = torch.full((rows, 2 * P), -1, dtype=torch.int16, device=cuda)
+    for out, ldo, od in ((f32, P, L.F32), (s3, 2 * P, L.BF16X3)):
         L.check(L.lib.vtd_extract_patches(img.data_ptr(), 2, H, W, 3, p, out.data_ptr(), ldo, od,
                                           L.stream_ptr()), "patches")
     torch.cuda.synchronize()
@@ -217,14 +235,27 @@ def test_patches_split_output(L, cuda, H, W, p, P):
 
 def test_split_arguments_validated(L, cuda):
     x = torch.zeros(4, 64, device=cuda)
-    y = torch.zeros(4, 190, dtype=torch.int16, device=cuda)
-    assert L.lib.vtd_split_bf16x3(x.data_ptr(), 4, 64, 64, y.data_ptr(), 190, 0, None) == -1
-    assert L.lib.vtd_split_bf16x3(x.data_ptr(), 4, 64, 64, y.data_ptr(), 180, 0, None) == -1
-    assert L.lib.vtd_split_bf16x3(x.data_ptr(), 4, 64, 64, y.data_ptr(), 192, 2, None) == -1
-    out = torch.zeros(4, 190, dtype=torch.int16, device=cuda)
-    e = _epi(L, out, 190, L.BF16X3)
+    y = torch.zeros(4, 192, dtype=torch.int16, device=cuda)
+    split = L.lib.vtd_split_bf16x3
+    assert split(x.data_ptr(), 4, 64, 64, y.data_ptr(), 129, 0, None) == -1   # 2 P, odd
+    assert split(x.data_ptr(), 4, 64, 64, y.data_ptr(), 120, 0, None) == -1   # P < K
+    assert split(x.data_ptr(), 4, 64, 64, y.data_ptr(), 190, 1, None) == -1   # 3 P
+    assert split(x.data_ptr(), 4, 64, 64, y.data_ptr(), 180, 1, None) == -1   # P < K
+    assert split(x.data_ptr(), 4, 64, 64, y.data_ptr(), 192, 2, None) == -1   # role
+    out = torch.zeros(4, 192, dtype=torch.int16, device=cuda)
+    e = _epi(L, out, 191, L.BF16X3)
+    assert L.lib.vtd_gemm(4, 64, 64, x.data_ptr(), 64, x.data_ptr(), 64, L.BF16, ctypes.byref(e),
+                          None) == -1            # split output: ldo % 2
+    e = _epi(L, out, 192, L.BF16X3)
     assert L.lib.vtd_gemm(4, 64, 64, x.data_ptr(), 64, x.data_ptr(), 64, L.F32, ctypes.byref(e),
                           None) == -1            # split output needs bf16 operands
+    f = torch.zeros(4, 64, device=cuda)
+    e = _epi(L, f, 64, L.F32)
+    gemm = L.lib.vtd_gemm
+    assert gemm(4, 64, 128, x.data_ptr(), 128, x.data_ptr(), 128, L.BF16X3, ctypes.byref(e),
+                None) == -1                      # split A: K = 3 P
+    assert gemm(4, 64, 192, x.data_ptr(), 120, x.data_ptr(), 192, L.BF16X3, ctypes.byref(e),
+                None) == -1                      # split A: lda >= 2 P
 
 
 def _attn_ref64(qkv, B, N, H, dk, dkp):
@@ -243,7 +274,7 @@ def test_attention_split_vs_fp64(L, cuda, B, N, H, dk):
     """vtd_attention with dtype VTD_BF16X3 (vtd.py:364-369 in the split-bf16 parity mode): f32
     query / key / value in, every product as hi.hi + lo.hi + hi.lo on the bf16 MFMA with fp32
     softmax statistics, the output written as the attention-output Dense's split-bf16 A operand
-    [hi | lo | hi].  hi + lo against the fp64 attention of the same f32 inputs: within 2e-5
+    [hi | lo].  hi + lo against the fp64 attention of the same f32 inputs: within 2e-5
     of max |O| (the f32 kernel's bound in test_gpu_kernels.test_attention)."""
     dkp = 32 if dk <= 32 else (64 if dk <= 64 else 128)
     ld = 3 * H * dkp + 8
@@ -254,15 +285,15 @@ def test_attention_split_vs_fp64(L, cuda, B, N, H, dk):
             c0 = part * H * dkp + h * dkp
             qkv[:, c0:c0 + dk] = g.normal(0, 1.5, size=(B * N, dk))
     P = H * dkp + 64
-    out = torch.full((B * N, 3 * P), -1, dtype=torch.int16, device=cuda)
+    out = torch.full((B * N, 2 * P), -1, dtype=torch.int16, device=cuda)
     qkv_d = torch.from_numpy(qkv).to(cuda)
     L.check(L.lib.vtd_attention(qkv_d.data_ptr(), B, N, H, dkp, ld, 1.0 / math.sqrt(dk),
-                                out.data_ptr(), 3 * P, L.BF16X3, L.stream_ptr()), "attention")
+                                out.data_ptr(), 2 * P, L.BF16X3, L.stream_ptr()), "attention")
     torch.cuda.synchronize()
     got = as_u16(out)
     inner = H * dkp
-    assert np.array_equal(got[:, 2 * P:2 * P + inner], got[:, :inner])   # third piece = hi
     assert (got[:, inner:P] == 0xFFFF).all()                              # not written
+    assert (got[:, P + inner:] == 0xFFFF).all()
     hi = bf16_to_f32(got[:, :inner]).astype(np.float64)
     lo = bf16_to_f32(got[:, P:P + inner]).astype(np.float64)
     # the lo piece is the split of the f32 value hi + lo: |lo| <= half an ulp of bf16(hi)
@@ -275,8 +306,8 @@ def test_attention_split_vs_fp64(L, cuda, B, N, H, dk):
 
 def test_attention_split_arguments_validated(L, cuda):
     x = torch.zeros(196, 3 * 64, device=cuda)
-    y = torch.zeros(196, 3 * 64 + 1, dtype=torch.int16, device=cuda)
-    assert L.lib.vtd_attention(x.data_ptr(), 1, 196, 1, 64, 192, 0.125, y.data_ptr(), 193,
-                               L.BF16X3, None) == -1        # ldo % 3 != 0
+    y = torch.zeros(196, 2 * 64 + 1, dtype=torch.int16, device=cuda)
+    assert L.lib.vtd_attention(x.data_ptr(), 1, 196, 1, 64, 192, 0.125, y.data_ptr(), 129,
+                               L.BF16X3, None) == -1        # ldo % 2 != 0
     assert L.lib.vtd_attention(x.data_ptr(), 1, 196, 1, 64, 192, 0.125, y.data_ptr(), 96,
                                L.BF16X3, None) == -1        # piece narrower than heads * dkp

@@ -825,8 +825,9 @@ def test_gemm_splitk(L, cuda, M, N, K, ksplit, act, out_dtype):
     e = L.VtdEpilogue()
     e.bias, e.act, e.out, e.ldo, e.out_dtype = L.ptr(bias), act, L.ptr(out), N, out_dtype
     e.resid, e.ldr = L.ptr(resid), (N if resid is not None else 0)
-    L.check(L.lib.vtd_gemm_splitk(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, ctypes.byref(e),
-                                  part.data_ptr(), part.numel() * 4, ksplit, L.stream_ptr()),
+    L.check(L.lib.vtd_gemm_splitk(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, L.BF16,
+                                  ctypes.byref(e), part.data_ptr(), part.numel() * 4, ksplit,
+                                  L.stream_ptr()),
             "vtd_gemm_splitk")
     torch.cuda.synchronize()
     ref64 = _np_act(act, (A.double() @ Bt.double().T + bias.double()).cpu().numpy())
@@ -856,8 +857,8 @@ def test_gemm_splitk_choice_and_args(L, cuda):
     e = L.VtdEpilogue()
     for ks, nbytes, K in ((1, 1 << 30, 512), (2, 16, 512), (9, 1 << 30, 512)):
         with pytest.raises(ValueError):
-            L.check(L.lib.vtd_gemm_splitk(64, 64, K, 1, K, 1, K, ctypes.byref(e), 1, nbytes, ks,
-                                          L.stream_ptr()), "gemm_splitk")
+            L.check(L.lib.vtd_gemm_splitk(64, 64, K, 1, K, 1, K, L.BF16, ctypes.byref(e), 1,
+                                          nbytes, ks, L.stream_ptr()), "gemm_splitk")
 
 
 def test_gemm_statout_needs_a_specialised_epilogue(L, cuda):

@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--variants", default="-1")
     ap.add_argument("--rounds", type=int, default=1)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32", "x3"],
-                    help="x3: the split-bf16 kernel (f32 qkv in, [hi | lo | hi] out)")
+                    help="x3: the split-bf16 kernel (f32 qkv in, [hi | lo] out)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     B, N, H, dkp = a.B, a.N, a.H, 64
@@ -34,7 +34,7 @@ def main():
     qkv = torch.randn(B * N, ld, generator=g, device=dev) * 1.5
     if a.dtype == "bf16":
         qkv = qkv.to(torch.bfloat16)
-    ldo = 3 * H * dkp if a.dtype == "x3" else H * dkp
+    ldo = 2 * H * dkp if a.dtype == "x3" else H * dkp
     out = torch.empty(B * N, ldo, device=dev,
                       dtype=torch.float32 if a.dtype == "f32" else torch.bfloat16)
     junk = torch.empty(512 << 20, dtype=torch.uint8, device=dev) if a.flush else None

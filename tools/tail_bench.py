@@ -53,7 +53,7 @@ def main():
                                                         L.BF16, ctypes.byref(epi(0)), st))}
         for ks in (2, 3, 4):
             calls[f"splitk{ks}"] = (lambda ks=ks: L.check(L.lib.vtd_gemm_splitk(
-                M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, ctypes.byref(epi(0)), part.data_ptr(),
+                M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, L.BF16, ctypes.byref(epi(0)), part.data_ptr(),
                 part.numel() * 4, ks, st)))
         # leading m-tiles: whole rounds of 256 tiles; the rest split-K near one round
         full = (tm * tn) // 256
@@ -67,7 +67,7 @@ def main():
 
                 def tail(ks=ks, r0=r0, m_rem=m_rem, m_main=m_main):
                     L.check(L.lib.vtd_gemm_splitk(m_rem * 256, N, K, A.data_ptr() + r0 * K * 2, K,
-                                                  Bt.data_ptr(), K, ctypes.byref(epi(r0)),
+                                                  Bt.data_ptr(), K, L.BF16, ctypes.byref(epi(r0)),
                                                   part.data_ptr(), part.numel() * 4, ks, st))
                     L.check(L.lib.vtd_gemm(m_main * 256, N, K, A.data_ptr(), K, Bt.data_ptr(), K,
                                            L.BF16, ctypes.byref(epi(0)), st))

@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must precede loading libvtd.so, see module doc)
 LIB_PATH = os.environ.get("VTD_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                           "libvtd.so")
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 KALIGN = 64
 MAX_MLP = 16
 MAX_HEAD = 64
@@ -96,7 +96,7 @@ SIGNATURES = {
                                     c_int, c_int, c_void_p]),
     "vtd_gemm": (c_int, [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int,
                          ctypes.POINTER(VtdEpilogue), c_void_p]),
-    "vtd_gemm_splitk": (c_int, [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int,
+    "vtd_gemm_splitk": (c_int, [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int,
                                 ctypes.POINTER(VtdEpilogue), c_void_p, c_size_t, c_int, c_void_p]),
     "vtd_gemm_splitk_choice": (c_int, [c_int, c_int, c_int, c_int]),
     "vtd_quantize_mx8": (c_int, [c_void_p, c_int, c_int64, c_int, c_int, c_int, c_void_p, c_int,

@@ -1407,7 +1407,7 @@ int launch_bf16_fl(const void* qkv, int B, int N, int heads, int ldqkv, float sc
 // softmax); the split of K / V happens once per workgroup, in the staging write (hi and lo
 // planes with the bf16 kernel's row strides, so the K reads and the V^T tr-reads are the
 // bf16 kernel's).  The output is written directly as the attention_output GEMM's split-bf16
-// A operand [hi | lo | hi] (three P = ldo / 3 wide pieces), so no split pass follows it.
+// A operand [hi | lo] (two P = ldo / 2 wide pieces), so no split pass follows it.
 template <int DKP>
 struct AttnX3Cfg {
   static constexpr int KC = 64;                       // keys per chunk
@@ -1453,7 +1453,7 @@ __global__ __launch_bounds__(64 * NWG, 1) void attention_x3_kernel(
   const int64_t row0 = (int64_t)b * N;
   const int q0 = (qb * NWG + wave) * 32;
   const bool active = q0 < N;
-  const int P = ldo / 3;               // piece width of the split output
+  const int P = ldo / 2;               // piece width of the split output
 
   bf16x8 qh[C::KSTEPS], ql[C::KSTEPS];
   {
@@ -1643,7 +1643,6 @@ __global__ __launch_bounds__(64 * NWG, 1) void attention_x3_kernel(
         const i32x4 lv = *reinterpret_cast<const i32x4*>(wst + 32 * 144 + r * 144 + ch * 16);
         *reinterpret_cast<i32x4*>(op) = hv;
         *reinterpret_cast<i32x4*>(op + P) = lv;
-        *reinterpret_cast<i32x4*>(op + 2 * P) = hv;
       }
     }
     return;
@@ -1662,7 +1661,6 @@ __global__ __launch_bounds__(64 * NWG, 1) void attention_x3_kernel(
       const uint2 hv = {h0, h1}, lv = {pack_lo_bf16x2(a, bb, h0), pack_lo_bf16x2(cc, dd, h1)};
       *reinterpret_cast<uint2*>(op + d) = hv;
       *reinterpret_cast<uint2*>(op + P + d) = lv;
-      *reinterpret_cast<uint2*>(op + 2 * P + d) = hv;
     }
 }
 
@@ -1741,10 +1739,10 @@ int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqk
   VTD_CHECK_ARG(dkp == 32 || dkp == 64 || dkp == 128, "attention: dkp must be 32/64/128");
   VTD_CHECK_ARG(dtype == VTD_F32 || dtype == VTD_BF16 || dtype == VTD_BF16X3,
                 "attention: bad dtype");
-  // VTD_BF16X3: f32 qkv in, the split-bf16 operand [hi | lo | hi] out (ldo = 3 P, P >= inner)
-  const int owidth = dtype == VTD_BF16X3 ? ldo / 3 : ldo;
-  VTD_CHECK_ARG(dtype != VTD_BF16X3 || ldo % 3 == 0,
-                "attention: a split-bf16 output needs ldo % 3 == 0");
+  // VTD_BF16X3: f32 qkv in, the split-bf16 operand [hi | lo] out (ldo = 2 P, P >= inner)
+  const int owidth = dtype == VTD_BF16X3 ? ldo / 2 : ldo;
+  VTD_CHECK_ARG(dtype != VTD_BF16X3 || ldo % 2 == 0,
+                "attention: a split-bf16 output needs ldo % 2 == 0");
   VTD_CHECK_ARG(ldqkv >= 3 * heads * dkp && owidth >= heads * dkp,
                 "attention: leading dimensions too small");
   VTD_CHECK_ARG(ldqkv % 8 == 0 && owidth % 8 == 0, "attention: ld must be multiple of 8");

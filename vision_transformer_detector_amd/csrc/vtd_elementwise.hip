@@ -22,22 +22,20 @@ __device__ __forceinline__ void st4(bf16_t* p, f32x4 v) {
   *reinterpret_cast<uint2*>(p) = uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
 }
 
-// split-bf16 output (VTD_BF16X3 A operand): [hi | lo | hi] at p, p + P, p + 2 P
+// split-bf16 output (VTD_BF16X3 A operand): [hi | lo] at p, p + P
 __device__ __forceinline__ void st4x3(bf16_t* p, int P, f32x4 v) {
   const uint32_t h0 = pack_bf16x2(v[0], v[1]), h1 = pack_bf16x2(v[2], v[3]);
   const uint2 hi = {h0, h1}, lo = {pack_lo_bf16x2(v[0], v[1], h0), pack_lo_bf16x2(v[2], v[3], h1)};
   *reinterpret_cast<uint2*>(p) = hi;
   *reinterpret_cast<uint2*>(p + P) = lo;
-  *reinterpret_cast<uint2*>(p + 2 * P) = hi;
 }
-// one element of a row of width ldy: plain, or split over three ldy / 3 wide pieces (X3)
+// one element of a row of width ldy: plain, or split over two ldy / 2 wide pieces (X3)
 template <bool X3, typename TO>
 __device__ __forceinline__ void st1(TO* yr, int c, int P, float v) {
   if constexpr (X3) {
     const bf16_t h = f32_to_bf16(v);
     yr[c] = h;
     yr[P + c] = lo_bf16(v, h);
-    yr[2 * P + c] = h;
   } else {
     yr[c] = DT<TO>::from(v);
   }
@@ -49,13 +47,13 @@ __device__ __forceinline__ void st4v(TO* p, int P, f32x4 v) {
 }
 
 // TI: the residual stream's dtype (f32, or bf16 in the bf16 / fp8 modes); TO: output.
-// X3: TO = bf16_t and the output is the split-bf16 operand, three ldy / 3 wide pieces.
+// X3: TO = bf16_t and the output is the split-bf16 operand, two ldy / 2 wide pieces.
 template <typename TI, typename TO, int NV, bool X3 = false>
 __global__ __launch_bounds__(256) void layernorm_kernel(
     const TI* __restrict__ x, int64_t rows, int D, int ldx,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
     TO* __restrict__ y, int ldy) {
-  const int P = X3 ? ldy / 3 : ldy;
+  const int P = X3 ? ldy / 2 : ldy;
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -105,7 +103,7 @@ __global__ __launch_bounds__(256) void layernorm_generic_kernel(
     const TI* __restrict__ x, int64_t rows, int D, int ldx,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
     TO* __restrict__ y, int ldy) {
-  const int P = X3 ? ldy / 3 : ldy;
+  const int P = X3 ? ldy / 2 : ldy;
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -206,7 +204,7 @@ template <typename TI, typename TO, int NC, int RPW, bool X3 = false>
 __global__ __launch_bounds__(256) void layernorm16_kernel(
     const TI* __restrict__ x, int64_t rows, int D, int ldx, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, TO* __restrict__ y, int ldy) {
-  const int P = X3 ? ldy / 3 : ldy;
+  const int P = X3 ? ldy / 2 : ldy;
   const int lane = threadIdx.x & 63;
   const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
   if (row0 >= rows) return;
@@ -295,7 +293,7 @@ int ln_dispatch(const void* xv, int64_t rows, int D, int ldx, const float* g,
   const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   const TI* x = static_cast<const TI*>(xv);
   TO* yo = static_cast<TO*>(y);
-  const bool vec = (D % 4 == 0) && (ldx % 4 == 0) && ((X3 ? ldy / 3 : ldy) % 4 == 0) &&
+  const bool vec = (D % 4 == 0) && (ldx % 4 == 0) && ((X3 ? ldy / 2 : ldy) % 4 == 0) &&
                    (reinterpret_cast<uintptr_t>(x) % (4 * sizeof(TI)) == 0) &&
                    (reinterpret_cast<uintptr_t>(y) % (4 * sizeof(TO)) == 0) &&
                    (reinterpret_cast<uintptr_t>(g) % 16 == 0) &&
@@ -606,12 +604,12 @@ __global__ __launch_bounds__(256) void fold_ln_kernel(const float* __restrict__ 
 // tf.image.extract_patches(SAME, size = stride = p) + Reshape: output row m = b*N + t
 // (t = gy*gw + gx), column k = (kh*p + kw)*C + c; outside the image -> 0.
 // Each thread writes 8 consecutive output columns (one 16-B bf16 / 32-B f32 store).
-// X3: TO = bf16_t, the split-bf16 operand (three ldo / 3 wide pieces)
+// X3: TO = bf16_t, the split-bf16 operand (two ldo / 2 wide pieces)
 template <typename TO, bool X3 = false>
 __global__ __launch_bounds__(256) void patches_kernel(
     const float* __restrict__ img, int B, int H, int W, int C, int p, int gw, int N,
     int top, int left, int P, TO* __restrict__ out, int ldo) {
-  const int pw = X3 ? ldo / 3 : ldo;          // width of one piece
+  const int pw = X3 ? ldo / 2 : ldo;          // width of one piece
   const int chunks = pw / 8;
   const int64_t total = (int64_t)B * N * chunks;
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
@@ -643,7 +641,6 @@ __global__ __launch_bounds__(256) void patches_kernel(
       hi.w = pack_bf16x2(v[6], v[7]); lo.w = pack_lo_bf16x2(v[6], v[7], hi.w);
       *reinterpret_cast<uint4*>(o) = hi;
       *reinterpret_cast<uint4*>(o + pw) = lo;
-      *reinterpret_cast<uint4*>(o + 2 * pw) = hi;
     } else if constexpr (sizeof(TO) == 2) {
       bf16x8 w;
 #pragma unroll
@@ -682,15 +679,15 @@ __global__ __launch_bounds__(256) void patches_dense_kernel(
 }
 
 // ------------------------------------------------------------------ split-bf16
-// f32 x [rows][ldx] (K columns) -> split-bf16 y [rows][ldy], three P = ldy / 3 wide pieces:
-// role 0 [hi | lo | hi] (A operand), role 1 [hi | hi | lo] (B operand); each thread 8 columns
-// of one row (16-B stores; columns [K, P) zero).  VEC: K % 8 == 0, ldx % 4 == 0, 16-B bases.
+// f32 x [rows][ldx] (K columns) -> split-bf16 y [rows][ldy]: role 0 [hi | lo] (A operand,
+// P = ldy / 2), role 1 [hi | hi | lo] (B operand, P = ldy / 3); each thread 8 columns of one
+// row (16-B stores; columns [K, P) zero).  VEC: K % 8 == 0, ldx % 4 == 0, 16-B bases.
 template <bool VEC>
 __global__ __launch_bounds__(256) void split_bf16x3_kernel(const float* __restrict__ x,
                                                            int64_t rows, int K, int ldx,
                                                            bf16_t* __restrict__ y, int ldy,
                                                            int role) {
-  const int P = ldy / 3, chunks = (P + 7) / 8;
+  const int P = role ? ldy / 3 : ldy / 2, chunks = (P + 7) / 8;
   const int64_t total = rows * chunks;
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
        g += (int64_t)gridDim.x * blockDim.x) {
@@ -699,7 +696,7 @@ __global__ __launch_bounds__(256) void split_bf16x3_kernel(const float* __restri
     const float* xr = x + m * ldx;
     bf16_t* yr = y + m * ldy;
     bf16_t* const pc1 = yr + P;                      // second piece
-    bf16_t* const pc2 = yr + 2 * P;                  // third piece
+    bf16_t* const pc2 = yr + 2 * P;                  // third piece (role 1)
     if (VEC && c0 + 8 <= P) {
       f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = a;
       if (c0 < K) {                                  // K % 8 == 0: all 8 or none
@@ -713,14 +710,14 @@ __global__ __launch_bounds__(256) void split_bf16x3_kernel(const float* __restri
       hi.w = pack_bf16x2(b[2], b[3]); lo.w = pack_lo_bf16x2(b[2], b[3], hi.w);
       *reinterpret_cast<uint4*>(yr + c0) = hi;
       *reinterpret_cast<uint4*>(pc1 + c0) = role ? hi : lo;
-      *reinterpret_cast<uint4*>(pc2 + c0) = role ? lo : hi;
+      if (role) *reinterpret_cast<uint4*>(pc2 + c0) = lo;
     } else {
       for (int c = c0; c < min(c0 + 8, P); ++c) {
         const float v = c < K ? xr[c] : 0.f;
         const bf16_t h = f32_to_bf16(v), l = lo_bf16(v, h);
         yr[c] = h;
         pc1[c] = role ? h : l;
-        pc2[c] = role ? l : h;
+        if (role) pc2[c] = l;
       }
     }
   }
@@ -787,8 +784,8 @@ int layernorm_launch(const void* x, int x_dtype, int64_t rows, int D, int ldx, c
   VTD_CHECK_ARG(dtype == VTD_F32 || dtype == VTD_BF16 || dtype == VTD_BF16X3,
                 "layernorm: bad dtype");
   VTD_CHECK_ARG(x_dtype == VTD_F32 || x_dtype == VTD_BF16, "layernorm: bad x dtype");
-  VTD_CHECK_ARG(dtype != VTD_BF16X3 || (ldy % 3 == 0 && ldy / 3 >= D),
-                "layernorm: a split-bf16 output needs ldy % 3 == 0 and ldy / 3 >= D");
+  VTD_CHECK_ARG(dtype != VTD_BF16X3 || (ldy % 2 == 0 && ldy / 2 >= D),
+                "layernorm: a split-bf16 output needs ldy % 2 == 0 and ldy / 2 >= D");
   ProfScope ps(st, PROF_LN, 0.0);
   if (dtype == VTD_BF16X3)
     return x_dtype == VTD_BF16
@@ -930,13 +927,13 @@ int patches_launch(const float* img, int B, int H, int W, int C, int p, void* ou
   VTD_CHECK_ARG(dtype == VTD_F32 || dtype == VTD_BF16 || dtype == VTD_BF16X3,
                 "extract_patches: bad dtype");
   if (dtype == VTD_BF16X3)
-    VTD_CHECK_ARG(ldo % 24 == 0 && ldo / 3 >= P,
-                  "extract_patches: a split-bf16 output needs ld_out % 24 == 0, ld_out / 3 >= P");
+    VTD_CHECK_ARG(ldo % 16 == 0 && ldo / 2 >= P,
+                  "extract_patches: a split-bf16 output needs ld_out % 16 == 0, ld_out / 2 >= P");
   else
     VTD_CHECK_ARG(ldo >= P && ldo % 8 == 0, "extract_patches: ld_out must be >= P, % 8");
   const int pad_h = (gh - 1) * p + p - H, pad_w = (gw - 1) * p + p - W;
   const int N = gh * gw;
-  const int64_t total = (int64_t)B * N * ((dtype == VTD_BF16X3 ? ldo / 3 : ldo) / 8);
+  const int64_t total = (int64_t)B * N * ((dtype == VTD_BF16X3 ? ldo / 2 : ldo) / 8);
   const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
   ProfScope ps(st, PROF_PATCH, 0.0);
   if (dtype == VTD_BF16 && pad_h == 0 && pad_w == 0 && (p * C) % 8 == 0 && ldo == P &&
@@ -962,10 +959,12 @@ int patches_launch(const float* img, int B, int H, int W, int C, int p, void* ou
 int split_bf16x3_launch(const float* x, int64_t rows, int K, int ldx, void* y, int ldy, int role,
                         hipStream_t st) {
   VTD_CHECK_ARG(x && y && rows > 0 && K > 0 && ldx >= K, "split_bf16x3: bad arguments");
-  VTD_CHECK_ARG(ldy % 3 == 0 && ldy / 3 >= K && (role == 0 || role == 1),
-                "split_bf16x3: ldy % 3 == 0, ldy / 3 >= K, role 0 or 1");
+  VTD_CHECK_ARG(role == 0 || role == 1, "split_bf16x3: role 0 or 1");
+  const int np = role ? 3 : 2;                       // pieces
+  VTD_CHECK_ARG(ldy % np == 0 && ldy / np >= K,
+                "split_bf16x3: ldy = 2 P (role 0) or 3 P (role 1) with P >= K");
   ProfScope ps(st, PROF_OTHER, 0.0);
-  const int P = ldy / 3;
+  const int P = ldy / np;
   const int64_t total = rows * ((P + 7) / 8);
   const int grid = (int)std::min<int64_t>((total + 255) / 256, 16384);
   const bool vec = K % 8 == 0 && ldx % 4 == 0 && P % 8 == 0 &&

@@ -36,11 +36,12 @@ __device__ __forceinline__ int swz(int row, int chunk) {
 
 __device__ __forceinline__ void gload4(i32x4 (&ra)[4], i32x4 (&rb)[4], const char* ga,
                                        const char* gb, const int64_t (&offa)[4],
-                                       const int64_t (&offb)[4], int kt) {
-  const int64_t o = (int64_t)kt * KB;
+                                       const int64_t (&offb)[4], int kt, int aw) {
+  // A: the split-bf16 wrap (EpiArgs::aw) -- B reads K-step kt, A stored step kt or kt - aw
+  const int64_t o = (int64_t)kt * KB, oa = (int64_t)(kt >= aw ? kt - aw : kt) * KB;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    ra[i] = *reinterpret_cast<const i32x4*>(ga + offa[i] + o);
+    ra[i] = *reinterpret_cast<const i32x4*>(ga + offa[i] + oa);
     rb[i] = *reinterpret_cast<const i32x4*>(gb + offb[i] + o);
   }
 }
@@ -91,13 +92,13 @@ __global__ __launch_bounds__(NT) void gemm_tn_kernel(
   const int fr = lane & 15, fg = lane >> 4;
   const int nk = K * (int)sizeof(T) / KB;
 
-  gload4(ra_, rb_, ga, gb, offa, offb, 0);
+  gload4(ra_, rb_, ga, gb, offa, offb, 0, e.aw);
   swrite4(ra_, rb_, lds_a, lds_b, srow, schunk, 0);
   __syncthreads();
 
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < nk) gload4(ra_, rb_, ga, gb, offa, offb, kt + 1);
+    if (kt + 1 < nk) gload4(ra_, rb_, ga, gb, offa, offb, kt + 1, e.aw);
     const char* la = lds_a + buf * TILE_BYTES;
     const char* lb = lds_b + buf * TILE_BYTES;
 #pragma unroll
@@ -166,10 +167,13 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(int M, int N, int K,
   const int nks = K >> 5;                         // 32-wide K-steps
   const bf16_t* ap = A + (int64_t)min(m0 + fr, M - 1) * lda + 8 * g;
   i32x4 a0[SK_CH], a1[SK_CH];
+  const int aw2 = 2 * e.aw;                       // the split-bf16 A wrap in 32-wide steps
   auto load = [&](i32x4 (&a)[SK_CH], int s0) {
 #pragma unroll
-    for (int j = 0; j < SK_CH; ++j)   // past the end: re-read the last step (no branches)
-      a[j] = *reinterpret_cast<const i32x4*>(ap + min(s0 + j, nks - 1) * 32);
+    for (int j = 0; j < SK_CH; ++j) {  // past the end: re-read the last step (no branches)
+      const int sa = min(s0 + j, nks - 1);
+      a[j] = *reinterpret_cast<const i32x4*>(ap + (sa >= aw2 ? sa - aw2 : sa) * 32);
+    }
   };
   load(a0, 0);
   // Bt rows n0 .. n0 + 31: slab t = k / 64, row r, 16-B chunk c at t * 4096 + r * 128 + (c ^ (r & 7)) * 16.
@@ -292,7 +296,7 @@ __device__ __forceinline__ void lds_read4_b64(const void* p, float2 (&o)[4]) {
       : "memory");
 }
 // EPI_S3 (split-bf16 output): o = the hi words of v0, v1 already stored at idx; the lo
-// piece at idx + s3, hi again at idx + 2 s3 ([hi | lo | hi])
+// piece at idx + s3 ([hi | lo])
 __device__ __forceinline__ void store_s3(const EpiArgs& e, int64_t idx, const i32x4& o, f32x4 v0,
                                          f32x4 v1) {
   const i32x4 lo = {(int)pack_lo_bf16x2(v0[0], v0[1], (uint32_t)o[0]),
@@ -301,7 +305,6 @@ __device__ __forceinline__ void store_s3(const EpiArgs& e, int64_t idx, const i3
                     (int)pack_lo_bf16x2(v1[2], v1[3], (uint32_t)o[3])};
   bf16_t* p = static_cast<bf16_t*>(e.out) + idx;
   store_out16(p + e.s3, lo);
-  store_out16(p + 2 * e.s3, o);
 }
 // TRL: the accumulators are in the transposed layout (lane (fr, fg): row 16 i + fr, columns
 // 32 jp + 8 fg .. + 7 in acc[i][2 jp], acc[i][2 jp + 1]): staged with ds_write_b128
@@ -636,23 +639,40 @@ __device__ __forceinline__ int grp_tile_row(int g, int gr) {
 // DMA source addressing of one tile, from wave-uniform scalars only (the per-lane part,
 // row-in-piece and swizzled chunk, is rederived from the lane id at each issue): keeps
 // 8 x 64-bit per-lane pointers out of the K loop's register budget.
+// AW: the kernel may read a split-bf16 A operand (EpiArgs::aw) -- A's K-step of loop step kt
+// is kt + ak0, minus aw once past it; !AW: kt (k0 folded into A's base), no scalar arithmetic
+// per DMA issue (the bf16 forward's kernels: -0.14 % at C2, profiles/r06_awrap_ab.log)
 struct PP2BufSrc {
   __amdgpu_buffer_rsrc_t ra, rb;
   int off[4][2];
+  int ak0, aw;
 };
+template <bool AW>
+struct PP2Src : PP2BufSrc {};
+// the pp2 epilogue codes whose kernels take the wrap: the split-bf16 output, the f32-output
+// codes (the split-bf16 forward's query/key/value and residual layers), split-K partials and
+// the generic epilogue; a wrapped A operand never runs the other codes (pp2_code)
+constexpr bool pp2_wraps(int code) {
+  return code == EPI_GENERIC || (code & EPI_S3) != 0 || (code & 4) == 0;
+}
 
-template <bool TR, typename T = bf16_t>
-__device__ __forceinline__ void pp2b_sources(PP2BufSrc& s, const T* A, int lda, int M,
+template <bool TR, typename T = bf16_t, bool AW = true>
+__device__ __forceinline__ void pp2b_sources(PP2Src<AW>& s, const T* A, int lda, int M,
                                              const T* Bt, int ldb, int N, int m0, int n0,
-                                             int wave, int lane, int k0 = 0, bool valid = true) {
+                                             int wave, int lane, int k0 = 0, bool valid = true,
+                                             int aw = 0) {
   // records = bytes from the tile base to the end of the operand (clamped to 32 bits); all
   // offsets are in range because rows are clamped to the last valid row.  k0: first K
-  // element of the loop (split-K ranges), folded into the base.
+  // element of the loop (split-K ranges), folded into B's base; A's K-step offset instead
+  // (ak0: the split-bf16 wrap aw counts stored K-steps from the row start)
   constexpr int ES = (int)sizeof(T);
-  const int64_t ra_bytes = (int64_t)(M - m0) * lda * ES - ES * k0,
+  const int ka0 = AW ? 0 : k0;               // the K offset folded into A's base
+  const int64_t ra_bytes = (int64_t)(M - m0) * lda * ES - ES * ka0,
                 rb_bytes = (int64_t)(N - n0) * ldb * ES - ES * k0;
+  s.ak0 = AW ? k0 * ES / 128 : 0;
+  s.aw = AW ? aw : 0;
   // !valid: zero records -- every load out of range (no memory traffic)
-  s.ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(A + (int64_t)m0 * lda + k0), 0,
+  s.ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(A + (int64_t)m0 * lda + ka0), 0,
                                            valid ? (int)std::min<int64_t>(ra_bytes, 0x7fffffff) : 0,
                                            0x00020000);
   s.rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(Bt + (int64_t)n0 * ldb + k0), 0,
@@ -671,15 +691,20 @@ __device__ __forceinline__ void pp2b_sources(PP2BufSrc& s, const T* A, int lda, 
     }
 }
 
-template <int G>
+template <int G, bool AW>
 __device__ __forceinline__ void pp2_issue(char* smem, const PP2BufSrc& src, int wave, int kt,
                                           int stage) {
   char* dst = smem + stage * BSTAGE + G * 16384 + wave * 2 * 1024;
+  int ks = kt;
+  if constexpr (G < 2 && AW) {
+    ks += src.ak0;
+    ks = ks >= src.aw ? ks - src.aw : ks;
+  }
 #pragma unroll
   for (int j = 0; j < 2; ++j)
     __builtin_amdgcn_raw_ptr_buffer_load_lds(G < 2 ? src.ra : src.rb,
                                              (lds_void_t*)(dst + j * 1024), 16, src.off[G][j],
-                                             kt * 128, 0, 0);
+                                             ks * 128, 0, 0);
 }
 
 // pre: K-tile 0 was issued by the caller (pp2_prefetch, during the previous output tile's
@@ -687,23 +712,23 @@ __device__ __forceinline__ void pp2_issue(char* smem, const PP2BufSrc& src, int 
 // before K-tile 1 is loaded over it.
 // NB (diagnostic build, VTD_PP2_DG & 32, wrong outputs): the K loop's per-phase barriers
 // dropped -- the cost of the ping-pong synchronisation itself
-template <bool TR, bool F32 = false, bool NB = false>
-__device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, const PP2BufSrc& src,
+template <bool TR, bool F32 = false, bool NB = false, bool AW = true>
+__device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, const PP2Src<AW>& src,
                                              int nk, int wave, int wm, int wn, int fr, int fg,
                                              uint64_t* t_prologue = nullptr, bool pre = false) {
   // prologue: tile 0 complete, tile 1's X0/Y0/Y1 in flight
   if (!pre) {
-    pp2_issue<0>(smem, src, wave, 0, 0);
-    pp2_issue<2>(smem, src, wave, 0, 0);
-    pp2_issue<3>(smem, src, wave, 0, 0);
-    pp2_issue<1>(smem, src, wave, 0, 0);
+    pp2_issue<0, AW>(smem, src, wave, 0, 0);
+    pp2_issue<2, AW>(smem, src, wave, 0, 0);
+    pp2_issue<3, AW>(smem, src, wave, 0, 0);
+    pp2_issue<1, AW>(smem, src, wave, 0, 0);
   } else {
     pp_barrier();
   }
   if (nk > 1) {
-    pp2_issue<0>(smem, src, wave, 1, 1);
-    pp2_issue<2>(smem, src, wave, 1, 1);
-    pp2_issue<3>(smem, src, wave, 1, 1);
+    pp2_issue<0, AW>(smem, src, wave, 1, 1);
+    pp2_issue<2, AW>(smem, src, wave, 1, 1);
+    pp2_issue<3, AW>(smem, src, wave, 1, 1);
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -722,7 +747,7 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
     pp_load_a(a, st + 0 * 16384, ra, fr, fg);
     if constexpr (TR) pp_load_b_t(b0, st + 2 * 16384, rb, fr, fg);
     else pp_load_b(b0, st + 2 * 16384, rb, fr, fg);
-    if constexpr (n1) pp2_issue<1>(smem, src, wave, kt + 1, (kt + 1) & 1);
+    if constexpr (n1) pp2_issue<1, AW>(smem, src, wave, kt + 1, (kt + 1) & 1);
     if constexpr (n1) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (!NB) pp_barrier();
@@ -740,15 +765,15 @@ __device__ __forceinline__ void pp2_mainloop(f32x4 (&acc)[8][4], char* smem, con
     if constexpr (!NB) pp_barrier();
     // ---- P2
     pp_load_a(a, st + 1 * 16384, ra, fr, fg);
-    if constexpr (n2) pp2_issue<0>(smem, src, wave, kt + 2, kt & 1);
+    if constexpr (n2) pp2_issue<0, AW>(smem, src, wave, kt + 2, kt & 1);
     if constexpr (!NB) pp_barrier();
     if constexpr (TR) pp_mfma_t<4, 2, F32>(acc, a, b1);
     else pp_mfma<4, 2, F32>(acc, a, b1);
     if constexpr (!NB) pp_barrier();
     // ---- P3
     if constexpr (n2) {
-      pp2_issue<2>(smem, src, wave, kt + 2, kt & 1);
-      pp2_issue<3>(smem, src, wave, kt + 2, kt & 1);
+      pp2_issue<2, AW>(smem, src, wave, kt + 2, kt & 1);
+      pp2_issue<3, AW>(smem, src, wave, kt + 2, kt & 1);
       asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -789,20 +814,20 @@ __device__ __forceinline__ void pp_mfma32(f32x4 (&acc)[8][4], const bf16x8 (&a)[
 // windows open at 4t-1 (G0) / 4t (G1).  X0,Y0,Y1(t+2) overwrite tile t's, last read by G1 in
 // X(t), retired by 4t+1; the Y(t) windows open at 4t+1 / 4t+2.  RAW: every wave waits for its
 // own DMA before the barrier that opens the readers' window.
-template <bool TR, bool F32 = false>
+template <bool TR, bool F32 = false, bool AW = true>
 __device__ __forceinline__ void pp2_mainloop_2ph(f32x4 (&acc)[8][4], char* smem,
-                                                 const PP2BufSrc& src, int nk, int wave, int wm,
+                                                 const PP2Src<AW>& src, int nk, int wave, int wm,
                                                  int wn, int fr, int fg,
                                                  uint64_t* t_prologue = nullptr) {
   // prologue: X0,Y0,Y1,X1(0) complete; X0,Y0,Y1(1) in flight
-  pp2_issue<0>(smem, src, wave, 0, 0);
-  pp2_issue<2>(smem, src, wave, 0, 0);
-  pp2_issue<3>(smem, src, wave, 0, 0);
-  pp2_issue<1>(smem, src, wave, 0, 0);
+  pp2_issue<0, AW>(smem, src, wave, 0, 0);
+  pp2_issue<2, AW>(smem, src, wave, 0, 0);
+  pp2_issue<3, AW>(smem, src, wave, 0, 0);
+  pp2_issue<1, AW>(smem, src, wave, 0, 0);
   if (nk > 1) {
-    pp2_issue<0>(smem, src, wave, 1, 1);
-    pp2_issue<2>(smem, src, wave, 1, 1);
-    pp2_issue<3>(smem, src, wave, 1, 1);
+    pp2_issue<0, AW>(smem, src, wave, 1, 1);
+    pp2_issue<2, AW>(smem, src, wave, 1, 1);
+    pp2_issue<3, AW>(smem, src, wave, 1, 1);
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -825,7 +850,7 @@ __device__ __forceinline__ void pp2_mainloop_2ph(f32x4 (&acc)[8][4], char* smem,
       pp_load_b(b1, st + 3 * 16384, rb, fr, fg);
     }
     if constexpr (n1) {
-      pp2_issue<1>(smem, src, wave, kt + 1, (kt + 1) & 1);
+      pp2_issue<1, AW>(smem, src, wave, kt + 1, (kt + 1) & 1);
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -836,9 +861,9 @@ __device__ __forceinline__ void pp2_mainloop_2ph(f32x4 (&acc)[8][4], char* smem,
     // ---- Y
     pp_load_a(a, st + 1 * 16384, ra, fr, fg);
     if constexpr (n2) {
-      pp2_issue<0>(smem, src, wave, kt + 2, kt & 1);
-      pp2_issue<2>(smem, src, wave, kt + 2, kt & 1);
-      pp2_issue<3>(smem, src, wave, kt + 2, kt & 1);
+      pp2_issue<0, AW>(smem, src, wave, kt + 2, kt & 1);
+      pp2_issue<2, AW>(smem, src, wave, kt + 2, kt & 1);
+      pp2_issue<3, AW>(smem, src, wave, kt + 2, kt & 1);
       asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     } else {
       // last K-step: every LDS read retired before the barrier, so that G0, released
@@ -1056,8 +1081,8 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_kernel(
   const int nk_all = K / 64, nks = ksplit > 1 ? (nk_all + ksplit - 1) / ksplit : nk_all;
   const int k0 = split * nks, nk = min(nks, nk_all - k0);   // host: every split non-empty
   if (ksplit > 1) e.out = static_cast<float*>(e.out) + split * e.split_stride;
-  PP2BufSrc src;
-  pp2b_sources<TR>(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane, k0 * 64);
+  PP2Src<pp2_wraps(EPI)> src;
+  pp2b_sources<TR>(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane, k0 * 64, true, e.aw);
   // LayerNorm-fold row statistics of the wave's 128 rows: issued before the K loop (the
   // oldest vector-memory op, so the loop's counted waits retire it), used in the epilogue
   float2 lst[2] = {float2{0.f, 0.f}, float2{0.f, 0.f}};
@@ -1198,8 +1223,8 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_mt_kernel(
     const int fr = lane & 15, fg = lane >> 4;
     float* const ep = reinterpret_cast<float*>(epb) + wave * 32 * 68;
     float2* const lds_st = reinterpret_cast<float2*>(epb + 8 * 32 * 68 * 4) + wave * 128;
-    PP2BufSrc src;
-    pp2b_sources<TR>(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane, k0 * 64);
+    PP2Src<pp2_wraps(EPI)> src;
+    pp2b_sources<TR>(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane, k0 * 64, true, e.aw);
     // LayerNorm-fold row statistics of the wave's 128 rows: issued before the K loop (older
     // than the K loop's DMAs, so its counted waits retire them), used in the epilogue
     float2 lst[2] = {float2{0.f, 0.f}, float2{0.f, 0.f}};
@@ -1233,13 +1258,13 @@ __global__ __launch_bounds__(BNT) void gemm_tn_bf16_pp2_mt_kernel(
     // same instruction sequence on both paths keeps the compiler's counted waits for the
     // epilogue's own loads exact, instead of the minimum over a branch merge
     auto prefetch = [&]() {
-      PP2BufSrc nsrc;
+      PP2Src<pp2_wraps(EPI)> nsrc;
       pp2b_sources<TR>(nsrc, A, lda, M, Bt, ldb, N, tm2 * BBM, tn2 * BBN, wave, lane, k0 * 64,
-                       more);
-      pp2_issue<0>(smem, nsrc, wave, 0, 0);
-      pp2_issue<2>(smem, nsrc, wave, 0, 0);
-      pp2_issue<3>(smem, nsrc, wave, 0, 0);
-      pp2_issue<1>(smem, nsrc, wave, 0, 0);
+                       more, e.aw);
+      pp2_issue<0, pp2_wraps(EPI)>(smem, nsrc, wave, 0, 0);
+      pp2_issue<2, pp2_wraps(EPI)>(smem, nsrc, wave, 0, 0);
+      pp2_issue<3, pp2_wraps(EPI)>(smem, nsrc, wave, 0, 0);
+      pp2_issue<1, pp2_wraps(EPI)>(smem, nsrc, wave, 0, 0);
     };
     if constexpr ((DG & 8) != 0) {
 #pragma unroll
@@ -1296,7 +1321,7 @@ __global__ __launch_bounds__(BNT) void gemm_tn_f32_pp2_kernel(
   int tm, tn;
   tile_coords(tile, e.to, tm, tn);
   const int m0 = tm * BBM, n0 = tn * BBN;
-  PP2BufSrc src;
+  PP2Src<false> src;
   pp2b_sources<TR, float>(src, A, lda, M, Bt, ldb, N, m0, n0, wave, lane, 0);
   f32x4 acc[8][4];
 #pragma unroll
@@ -1631,7 +1656,7 @@ constexpr bool pp2_specialised(int code) {
 bool pp2_fast_epilogue(const vtd_epilogue* e) {
   auto al16 = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
   return e->bias && !e->detections && e->scatter_tokens <= 0 && e->ldo % 8 == 0 &&
-         (e->out_dtype != VTD_BF16X3 || (e->ldo / 3) % 8 == 0) &&
+         (e->out_dtype != VTD_BF16X3 || (e->ldo / 2) % 8 == 0) &&
          (!e->resid || e->ldr % 8 == 0) && al16(e->out) && al16(e->bias) &&
          (!e->resid || al16(e->resid)) && (!e->out2 || (e->ldo2 % 8 == 0 && al16(e->out2)));
 }
@@ -1817,6 +1842,17 @@ int gemm_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int
   return gemm_launch_ln(M, N, K, A, lda, Bt, ldb, dtype, epi, stream, flops, nullptr, 0, 0, 0.f);
 }
 
+// dtype VTD_BF16X3 (include/vtd.h "Split-bf16 operands"): a bf16 GEMM over K = 3 P whose A
+// rows are stored [hi | lo] (lda >= 2 P) and read as [hi | lo | hi] -- EpiArgs::aw = 2 P / 64
+// K-steps, after which the loop's A column returns to 0.  Returns aw (0: not split) and the
+// kernels' dtype (VTD_BF16) in dtype, or -1 when the shape cannot be split.
+int split_a_wrap(int& dtype, int K, int lda) {
+  if (dtype != VTD_BF16X3) return 0;
+  if (K % (3 * VTD_KALIGN) != 0 || lda < 2 * (K / 3)) return -1;
+  dtype = VTD_BF16;
+  return 2 * (K / 3) / 64;
+}
+
 // A GEMM whose LayerNorm-fold row statistics (epi->lnstat) are still the producer's partials
 // (lnpart, lnslots per row; the fold path): ln_stats_finalize first writes epi->lnstat.
 // lnpart == nullptr: a plain gemm_launch.
@@ -1826,16 +1862,20 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
   VTD_CHECK_ARG(M > 0 && N > 0 && K > 0, "gemm: M, N, K must be positive");
   VTD_CHECK_ARG(K % VTD_KALIGN == 0, "gemm: K must be a multiple of VTD_KALIGN");
   VTD_CHECK_ARG(A && Bt && epi && epi->out, "gemm: null pointer");
-  VTD_CHECK_ARG(lda >= K && ldb >= K && lda % 8 == 0 && ldb % 8 == 0,
+  VTD_CHECK_ARG(dtype == VTD_F32 || dtype == VTD_BF16 || dtype == VTD_BF16X3, "gemm: bad dtype");
+  const bool split_a = dtype == VTD_BF16X3;
+  const int aw = split_a_wrap(dtype, K, lda);
+  VTD_CHECK_ARG(aw >= 0, "gemm: a split-bf16 A operand needs K = 3 P with P % 64 == 0 and "
+                         "lda >= 2 P");
+  VTD_CHECK_ARG((split_a || lda >= K) && ldb >= K && lda % 8 == 0 && ldb % 8 == 0,
                 "gemm: lda/ldb must be >= K and multiples of 8");
-  VTD_CHECK_ARG(dtype == VTD_F32 || dtype == VTD_BF16, "gemm: bad dtype");
   VTD_CHECK_ARG(epi->out_dtype == VTD_F32 || epi->out_dtype == VTD_BF16 ||
                     (epi->out_dtype == VTD_BF16X3 && dtype == VTD_BF16),
                 "gemm: bad out dtype (VTD_BF16X3 output: bf16 operands only)");
   VTD_CHECK_ARG(epi->out_dtype != VTD_BF16X3 ||
-                    (epi->ldo % 3 == 0 && epi->ldo / 3 >= N && !epi->out2 && !epi->detections &&
+                    (epi->ldo % 2 == 0 && epi->ldo / 2 >= N && !epi->out2 && !epi->detections &&
                      !epi->resid && !epi->statout),
-                "gemm: a split-bf16 output needs ldo % 3 == 0, ldo / 3 >= N, no out2 / "
+                "gemm: a split-bf16 output needs ldo % 2 == 0, ldo / 2 >= N, no out2 / "
                 "detections / residual / statistics");
   VTD_CHECK_ARG(!epi->rowadd || epi->rowadd_period > 0, "gemm: rowadd_period");
   VTD_CHECK_ARG(epi->scatter_tokens <= 0 || N <= VTD_MAX_DETECT,
@@ -1862,7 +1902,7 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
     const bf16_t* b16 = static_cast<const bf16_t*>(Bt);
     const int ngw = tile_group_width(tiles_n);
 #if VTD_DIAG
-    if (gemm_variant() == 12 && epi->out_dtype != VTD_BF16X3) {   // (w4: no split output)
+    if (gemm_variant() == 12 && epi->out_dtype != VTD_BF16X3 && aw == 0) {   // (w4: no split)
       if (!gemm_w4_launch(M, N, K, a16, lda, b16, ldb, epi, ngw, stream))
         return fail(VTD_ERR_HIP, "gemm: w4 kernel attributes could not be set");
       VTD_LAUNCH_CHECK("gemm");
@@ -1871,6 +1911,7 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
 #endif
     pp2_set_attributes();
     EpiArgs e = make_epi_args(epi);
+    e.aw = aw;
     e.ngw = ngw;
     e.to = make_tile_order(tiles_m, tiles_n, e.ngw);
     e.tpw = VTD_DIAG ? pp2_tpw() : 1;   // several tiles per workgroup: diagnostic build only
@@ -1878,7 +1919,8 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
     static const int pp2_sleep = getenv("VTD_PP2_SLEEP") ? atoi(getenv("VTD_PP2_SLEEP")) : 0;
     e.dsl = pp2_sleep;
 #endif
-    const int code = pp2_code(epi);
+    // a wrapped (split-bf16) A operand: the codes whose kernels take the wrap (pp2_wraps)
+    const int code = aw > 0 && !pp2_wraps(pp2_code(epi)) ? EPI_GENERIC : pp2_code(epi);
     // transposed accumulators + register-direct epilogue for activation layers (mlp1 -5 %,
     // mlp2 -1.5 %), LDS-staged row vectors for the others (attn_out -10 %, mlp3 -4 %);
     // knob VTD_KNOB_GEMM_TR: 0 = never, 1 = always
@@ -1890,7 +1932,7 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
     // epilogue ablation (wrong outputs): VTD_PP2_DG = the DG bits of epilogue_fast /
     // epilogue_direct, for the plain / residual / statistics codes gemm_bench uses
     static const int pp2_dg = getenv("VTD_PP2_DG") ? atoi(getenv("VTD_PP2_DG")) : 0;
-    if (pp2_dg > 0) {
+    if (pp2_dg > 0 && aw == 0) {
       bool done = true;
       auto dg = [&](auto c) {
         constexpr int C = decltype(c)::value;
@@ -1950,7 +1992,8 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
     f32_pp2_launch(M, N, K, static_cast<const float*>(A), lda, static_cast<const float*>(Bt), ldb,
                    epi, tiles_m, tiles_n, stream);
   } else if (dtype == VTD_BF16 && K <= SK_KMAX && skinny_choice(M, N, K)) {
-    const EpiArgs e = make_epi_args(epi);
+    EpiArgs e = make_epi_args(epi);
+    e.aw = aw;
     const dim3 grid((M + SK_ROWS - 1) / SK_ROWS, (N + 31) / 32);
     const size_t lds = (size_t)32 * K * 2;
     static std::once_flag once[kMaxDevices];
@@ -1961,7 +2004,8 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
     hipLaunchKernelGGL(gemm_skinny_kernel, grid, dim3(256), lds, stream, M, N, K,
                        static_cast<const bf16_t*>(A), lda, static_cast<const bf16_t*>(Bt), ldb, e);
   } else {
-    const EpiArgs e = make_epi_args(epi);
+    EpiArgs e = make_epi_args(epi);
+    e.aw = aw;
     dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM);
     const size_t lds = 4 * TILE_BYTES;
     if (dtype == VTD_BF16)
@@ -1989,7 +2033,7 @@ int gemm_splitk_choice(int M, int N, int K, int dtype, int target) {
   // knob value >= 64: the workgroup target itself (A/B of the concurrent micro-batch halves);
   // target > 0: the caller's (vtd_forward: 256 / the concurrent parts)
   const int kSplitTarget = ks >= 64 ? ks : target > 0 ? target : kSplitTargetDefault;
-  if (dtype != VTD_BF16 || N <= 64 || K % 64 != 0 || M <= 0) return 1;
+  if ((dtype != VTD_BF16 && dtype != VTD_BF16X3) || N <= 64 || K % 64 != 0 || M <= 0) return 1;
   const int tiles = ((M + BBM - 1) / BBM) * ((N + BBN - 1) / BBN);
   const int nk = K / 64;
   if (tiles >= (3 * kSplitTarget) / 4) return 1;
@@ -2005,15 +2049,20 @@ int gemm_splitk_choice(int M, int N, int K, int dtype, int target) {
 // ([ksplit][M][N] floats), then gemm_splitk_epilogue_kernel.  Same products as the unsplit
 // kernels, summed in a different order (fp32).
 int gemm_splitk_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
-                       const vtd_epilogue* epi, float* part, int ksplit, hipStream_t stream,
-                       double flops) {
+                       int dtype, const vtd_epilogue* epi, float* part, int ksplit,
+                       hipStream_t stream, double flops) {
   VTD_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 64 == 0 && N % 4 == 0,
                 "gemm_splitk: M, N, K positive, K % 64, N % 4");
   VTD_CHECK_ARG(A && Bt && epi && epi->out && part, "gemm_splitk: null pointer");
+  VTD_CHECK_ARG(dtype == VTD_BF16 || dtype == VTD_BF16X3, "gemm_splitk: bf16 operands only");
+  const bool split_a = dtype == VTD_BF16X3;
+  const int aw = split_a_wrap(dtype, K, lda);
+  VTD_CHECK_ARG(aw >= 0, "gemm_splitk: a split-bf16 A operand needs K = 3 P with P % 64 == 0 "
+                         "and lda >= 2 P");
   // the reduce kernel reads the partials as 16-B vectors (N % 4 keeps every row aligned)
   VTD_CHECK_ARG(reinterpret_cast<uintptr_t>(part) % 16 == 0,
                 "gemm_splitk: part_dev must be 16-byte aligned");
-  VTD_CHECK_ARG(lda >= K && ldb >= K && lda % 8 == 0 && ldb % 8 == 0,
+  VTD_CHECK_ARG((split_a || lda >= K) && ldb >= K && lda % 8 == 0 && ldb % 8 == 0,
                 "gemm_splitk: lda/ldb must be >= K and multiples of 8");
   VTD_CHECK_ARG(ksplit >= 2 && ksplit <= K / 64, "gemm_splitk: ksplit");
   VTD_CHECK_ARG(!epi->statout && !epi->lnstat,
@@ -2028,6 +2077,7 @@ int gemm_splitk_launch(int M, int N, int K, const void* A, int lda, const void* 
   pe.ngw = tile_group_width(tiles_n);
   pe.to = make_tile_order(tiles_m, tiles_n, pe.ngw);
   pe.split_stride = (int64_t)M * N;
+  pe.aw = aw;
   const bf16_t* a16 = static_cast<const bf16_t*>(A);
   const bf16_t* b16 = static_cast<const bf16_t*>(Bt);
   const dim3 g(tiles_m * tiles_n * ksplit);
@@ -2168,11 +2218,11 @@ extern "C" int vtd_gemm_mx8(int M, int N, int K, const uint8_t* A_dev, int lda,
 }
 
 extern "C" int vtd_gemm_splitk(int M, int N, int K, const void* A_dev, int lda,
-                               const void* Bt_dev, int ldb, const vtd_epilogue* epi,
+                               const void* Bt_dev, int ldb, int dtype, const vtd_epilogue* epi,
                                float* part_dev, size_t part_bytes, int ksplit, void* stream) {
   if (ksplit < 2 || part_bytes < (size_t)ksplit * (size_t)std::max(M, 0) * std::max(N, 0) * 4)
     return vtd::fail(VTD_ERR_INVALID_ARG, "gemm_splitk: ksplit < 2 or part_bytes too small");
-  return vtd::gemm_splitk_launch(M, N, K, A_dev, lda, Bt_dev, ldb, epi, part_dev, ksplit,
+  return vtd::gemm_splitk_launch(M, N, K, A_dev, lda, Bt_dev, ldb, dtype, epi, part_dev, ksplit,
                                  static_cast<hipStream_t>(stream), 0.0);
 }
 

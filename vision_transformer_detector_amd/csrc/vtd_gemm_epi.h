@@ -82,8 +82,12 @@ struct EpiArgs {
   int tpw;
   // the tile order of ngw with precomputed divisors (set with ngw by the 256-tile launchers)
   TileOrder to;
-  // out_dtype VTD_BF16X3: width of one piece of the split-bf16 output row (ldo / 3)
+  // out_dtype VTD_BF16X3: width of one piece of the split-bf16 output row [hi | lo] (ldo / 2)
   int s3;
+  // split-bf16 A operand (dtype VTD_BF16X3): the stored row [hi | lo] is read as the K' = 3 P
+  // row [hi | lo | hi] -- K-step (64 wide) ka of the loop reads stored step ka, or ka - aw
+  // once ka >= aw (aw = 2 P / 64); 0 (no wrap: ka - 0) for every other operand
+  int aw;
   // diagnostic build only (VTD_PP2_SLEEP): first-round pp2 workgroups in odd XCD slots start
   // dsl x 512 cycles late (epilogue phases of neighbouring CUs out of step); 0 in the product
   int dsl;
@@ -253,12 +257,11 @@ __device__ __forceinline__ void epi_store(const EpiArgs& e, int M, int N, int m,
   }
   if (e.out_dtype == VTD_F32) {
     static_cast<float*>(e.out)[idx] = v;
-  } else if (e.out_dtype == VTD_BF16X3) {         // [hi | lo | hi]
+  } else if (e.out_dtype == VTD_BF16X3) {         // [hi | lo]
     bf16_t* o = static_cast<bf16_t*>(e.out) + idx;
     const bf16_t h = f32_to_bf16(v);
     o[0] = h;
     o[e.s3] = lo_bf16(v, h);
-    o[2 * e.s3] = h;
   } else {
     static_cast<bf16_t*>(e.out)[idx] = f32_to_bf16(v);
   }
@@ -311,7 +314,6 @@ __device__ __forceinline__ void epi_store4(const EpiArgs& e, int M, int N, int m
     *reinterpret_cast<uint2*>(o) = uint2{h0, h1};
     *reinterpret_cast<uint2*>(o + e.s3) =
         uint2{pack_lo_bf16x2(v[0], v[1], h0), pack_lo_bf16x2(v[2], v[3], h1)};
-    *reinterpret_cast<uint2*>(o + 2 * e.s3) = uint2{h0, h1};
   } else {
     bf16x4 o;
 #pragma unroll
@@ -337,8 +339,8 @@ constexpr int EPI_LNF = 32, EPI_STAT = 64, EPI_F8O = 128;
 // and the rare runtime modes: the position-embedding row add (patch embedding) and the bf16
 // copy of an f32 residual stream (out2)
 constexpr int EPI_RA = 256, EPI_O2 = 512;
-// the split-bf16 output (out_dtype VTD_BF16X3, with the bf16-output bit 4): [hi | lo | hi]
-// over three e.s3 wide pieces -- the next split-bf16 GEMM's A operand
+// the split-bf16 output (out_dtype VTD_BF16X3, with the bf16-output bit 4): [hi | lo] over
+// two e.s3 wide pieces -- the next split-bf16 GEMM's A operand
 constexpr int EPI_S3 = 1024;
 __host__ __device__ constexpr int epi_code(int act, bool out_bf16, bool resid) {
   return act | (out_bf16 ? 4 : 0) | (resid ? 8 : 0);
@@ -414,7 +416,8 @@ __host__ inline EpiArgs make_epi_args(const vtd_epilogue* epi) {
             epi->scatter_tokens, reinterpret_cast<const float2*>(epi->lnstat), epi->colsum,
             reinterpret_cast<float2*>(epi->statout), epi->stat_ld, epi->scale_out,
             epi->scale_rows, epi->detections};
-  e.s3 = epi->out_dtype == VTD_BF16X3 ? epi->ldo / 3 : 0;
+  e.s3 = epi->out_dtype == VTD_BF16X3 ? epi->ldo / 2 : 0;
+  e.aw = 0;
   return e;
 }
 

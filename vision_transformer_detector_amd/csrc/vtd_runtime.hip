@@ -28,8 +28,8 @@ int ln_stats_finalize_launch(const float* part, int64_t rows, int slots, int D, 
 bool gemm_emits_stats(int M, int N, int dtype, const vtd_epilogue* e);
 int gemm_splitk_choice(int M, int N, int K, int dtype, int target = 0);
 int gemm_splitk_launch(int M, int N, int K, const void* A, int lda, const void* Bt, int ldb,
-                       const vtd_epilogue* epi, float* part, int ksplit, hipStream_t stream,
-                       double flops);
+                       int dtype, const vtd_epilogue* epi, float* part, int ksplit,
+                       hipStream_t stream, double flops);
 int patches_launch(const float* img, int B, int H, int W, int C, int p, void* out, int ldo,
                    int dtype, hipStream_t st);
 int attention_mx8_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqkv,
@@ -214,8 +214,10 @@ int act_dtype(int dtype) {
 }
 size_t es_of(int dtype) { return act_dtype(dtype) == VTD_BF16 ? 2 : 4; }
 // GEMM A operands (patches, LayerNorm out, MLP / head activations): bytes per logical element
-// (VTD_BF16X3: three bf16 pieces) and the operand width of a K-wide logical row
-size_t eop_of(int dtype) { return dtype == VTD_BF16X3 ? 6 : es_of(dtype); }
+// (VTD_BF16X3: the two bf16 pieces [hi | lo]) and the stored width of a K-wide logical row;
+// opk: the GEMM's K (and the weights' row width) for it (VTD_BF16X3: K' = 3 K)
+size_t eop_of(int dtype) { return dtype == VTD_BF16X3 ? 4 : es_of(dtype); }
+int opa(int dtype, int k) { return dtype == VTD_BF16X3 ? 2 * k : k; }
 int opk(int dtype, int k) { return dtype == VTD_BF16X3 ? 3 * k : k; }
 // dtype of the residual stream x: bf16 in the bf16 / fp8 modes (the stream the GEMM
 // epilogues add into and the LayerNorms read), f32 in the f32 mode.  VTD_RESID_F32=1
@@ -283,7 +285,7 @@ Plan make_plan(const vtd_config* c, const vtd_dims& d, int nparts = 1) {
   size_t sk = 0;
   for (int j = 0, k = d.tokens_p; j < d.n_head; k = d.head_units_p[j], ++j) {
     const int s = gemm_splitk_choice((int)HR, d.head_units_p[j], opk(c->dtype, k),
-                                     c->dtype == VTD_BF16X3 ? VTD_BF16 : act_dtype(c->dtype),
+                                     c->dtype == VTD_BF16X3 ? VTD_BF16X3 : act_dtype(c->dtype),
                                      splitk_target(nparts));
     if (s > 1) sk = std::max(sk, (size_t)s * HR * d.head_units_p[j] * 4);
   }
@@ -537,11 +539,13 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   const bool pad = nparts > 1 && split_pad();
   const bool fp8 = cfg->dtype == VTD_FP8;
   const int dt = act_dtype(cfg->dtype);
-  // VTD_BF16X3: every GEMM runs on split-bf16 operands (bf16 kernels over K' = 3 K_p), whose
-  // A operands the producers write directly (odt); qkv / attention / x stay f32
+  // VTD_BF16X3: every GEMM runs on split-bf16 operands (bf16 kernels over K' = 3 K_p, A rows
+  // stored [hi | lo], 2 K_p wide: ka), whose A operands the producers write directly (odt);
+  // qkv / attention / x stay f32
   const bool x3 = cfg->dtype == VTD_BF16X3;
-  const int gdt = x3 ? VTD_BF16 : dt, odt = x3 ? VTD_BF16X3 : dt;
+  const int gdt = x3 ? VTD_BF16X3 : dt, odt = x3 ? VTD_BF16X3 : dt;
   auto kk = [&](int k) { return opk(cfg->dtype, k); };
+  auto ka = [&](int k) { return opa(cfg->dtype, k); };
   const int B = cfg->batch, N = d.tokens, D = d.d, Dp = d.d_p;
   // R: the encoder's rows (the real batch x tokens, or whole 256-row tiles of a part: pad)
   const int64_t R = gemm_rows(d, pad);
@@ -599,7 +603,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   // against the MX-fp8 weights (W [Np][K8], S [K8/128][Np][4])
   auto enc_gemm = [&](int Np, int K, const void* a, const void* W, const uint8_t* S,
                       const vtd_epilogue* e, double flops) -> int {
-    if (!fp8) return gemm_launch(M, Np, kk(K), a, kk(K), W, kk(K), gdt, e, st, flops);
+    if (!fp8) return gemm_launch(M, Np, kk(K), a, ka(K), W, kk(K), gdt, e, st, flops);
     const int K8 = k8_of(K);
     int r = quantize_mx8_launch(a, VTD_BF16, R, K, K, K8, q8, K8, s8, P.s8_rows, st);
     if (r) return r;
@@ -625,7 +629,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   if (s_lo <= 0 && 0 < s_hi) {
   // ---- ExtractImagePatches + flatten (vtd.py:271-280)
   rc = patches_launch(images, B, cfg->image_h, cfg->image_w, cfg->channels,
-                      cfg->patch_size, patches, kk(d.patch_dim_p), odt, st);
+                      cfg->patch_size, patches, ka(d.patch_dim_p), odt, st);
   if (rc) return rc;
   if (R > d.rows) {                                   // pad rows: zero patches
     const size_t row_bytes = (size_t)d.patch_dim_p * eop_of(cfg->dtype);
@@ -644,7 +648,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     e.act = VTD_ACT_NONE;
     e.out = x; e.ldo = Dp; e.out_dtype = rdt;
     emit_stats(e, cfg->repeat_times > 0 && w->layers[0].ln1_colsum);
-    rc = gemm_launch(M, Dp, kk(d.patch_dim_p), patches, kk(d.patch_dim_p), w->w_patch,
+    rc = gemm_launch(M, Dp, kk(d.patch_dim_p), patches, ka(d.patch_dim_p), w->w_patch,
                      kk(d.patch_dim_p), gdt, &e, st, 2.0 * fR * D * d.patch_dim);
     if (rc) return rc;
   }
@@ -654,8 +658,9 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   const int i_lo = std::max(s_lo - 1, 0), i_hi = std::min(s_hi - 1, cfg->repeat_times);
   for (int i = i_lo; i < i_hi; ++i) {                  // vtd.py:350-412
     const vtd_layer_weights& L = w->layers[i];
-    if (fp8 && (L.ln1_colsum || L.ln2_colsum))
-      return fail(VTD_ERR_UNSUPPORTED, "forward: LayerNorm fold (ln*_colsum) is not supported in VTD_FP8 mode");
+    if ((fp8 || x3) && (L.ln1_colsum || L.ln2_colsum))
+      return fail(VTD_ERR_UNSUPPORTED, "forward: LayerNorm fold (ln*_colsum) is not supported in "
+                                       "the VTD_FP8 / VTD_BF16X3 modes");
     // the folded GEMMs take the residual stream x itself as their A operand (read in dt)
     if (rdt != dt && (L.ln1_colsum || L.ln2_colsum))
       return fail(VTD_ERR_UNSUPPORTED, "forward: LayerNorm fold (ln*_colsum) needs the residual "
@@ -668,7 +673,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     } else if (fp8) {
       rc = ln_mx8(L.ln1_gamma, L.ln1_beta);       // LayerNorm + MX quantization, one pass
     } else {
-      rc = layernorm_launch(x, rdt, R, D, Dp, L.ln1_gamma, L.ln1_beta, 1e-3f, h, kk(Dp), odt, st);
+      rc = layernorm_launch(x, rdt, R, D, Dp, L.ln1_gamma, L.ln1_beta, 1e-3f, h, ka(Dp), odt, st);
     }
     if (rc) return rc;
     {
@@ -688,7 +693,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
          : attn_mx8 ? attention_mx8_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale,
                                          q8, d.inner_p, s8, P.s8_rows, st, attn_flops)
          : x3 ? attention_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale,
-                                 ws + P.attn3, kk(d.inner_p), VTD_BF16X3, st, attn_flops, nconc)
+                                 ws + P.attn3, ka(d.inner_p), VTD_BF16X3, st, attn_flops, nconc)
                   : attention_launch(qkv, B, N, cfg->num_heads, d.key_dim_p, d.qkv_p, scale,
                                      attn, d.inner_p, dt, st, attn_flops, nconc);
     if (rc) return rc;
@@ -716,7 +721,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
       rc = ln_mx8(L.ln2_gamma, L.ln2_beta);
       aq = q8; as = s8;
     } else {
-      rc = layernorm_launch(x, rdt, R, D, Dp, L.ln2_gamma, L.ln2_beta, 1e-3f, h, kk(Dp), odt, st);
+      rc = layernorm_launch(x, rdt, R, D, Dp, L.ln2_gamma, L.ln2_beta, 1e-3f, h, ka(Dp), odt, st);
     }
     if (rc) return rc;
     int k = Dp, kv = D;
@@ -733,7 +738,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
         }
         emit_stats(e, i + 1 < cfg->repeat_times && w->layers[i + 1].ln1_colsum);
       } else {
-        e.out = mlp[j & 1]; e.ldo = kk(d.mlp_units_p[j]); e.out_dtype = odt;
+        e.out = mlp[j & 1]; e.ldo = ka(d.mlp_units_p[j]); e.out_dtype = odt;
       }
       // VTD_FP8: an inner MLP layer writes the next layer's MX-fp8 operand itself (into the
       // operand buffer it is not reading) when every tile takes the fast epilogue
@@ -767,16 +772,16 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     VTD_HIP(hipMemsetAsync(u, 0, (size_t)d.head_rows * d.tokens_p * eop_of(cfg->dtype), st));
     vtd_epilogue e{};
     e.bias = w->b_det; e.act = VTD_ACT_NONE;
-    e.out = u; e.ldo = kk(d.tokens_p); e.out_dtype = odt;
+    e.out = u; e.ldo = ka(d.tokens_p); e.out_dtype = odt;
     e.scatter_tokens = N;
     const void* a = dt == rdt ? x : xb;
     if (x3) {                        // the f32 stream x as the split-bf16 operand (h is free)
-      rc = split_bf16x3_launch(static_cast<const float*>(x), R, Dp, Dp, h, kk(Dp), 0, st);
+      rc = split_bf16x3_launch(static_cast<const float*>(x), R, Dp, Dp, h, ka(Dp), 0, st);
       if (rc) return rc;
       a = h;
     }
     // the real rows only (the scatter addresses images by row)
-    rc = gemm_launch((int)d.rows, VTD_MAX_DETECT, kk(Dp), a, kk(Dp), w->w_det, kk(Dp), gdt, &e,
+    rc = gemm_launch((int)d.rows, VTD_MAX_DETECT, kk(Dp), a, ka(Dp), w->w_det, kk(Dp), gdt, &e,
                      st, 2.0 * fR * D * VTD_MAX_DETECT);
     if (rc) return rc;
   }
@@ -786,12 +791,12 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   for (int j = 0; j < d.n_head; ++j) {                // vtd.py:468-486
     vtd_epilogue e{};
     e.bias = w->b_head[j]; e.act = act;
-    e.out = head[j & 1]; e.ldo = kk(d.head_units_p[j]); e.out_dtype = odt;
+    e.out = head[j & 1]; e.ldo = ka(d.head_units_p[j]); e.out_dtype = odt;
     const double fl = 2.0 * HR * (double)kv * d.head_units[j];
     const int ks = gemm_splitk_choice(HR, d.head_units_p[j], kk(k), gdt, splitk_target(nparts));
-    rc = ks > 1 ? gemm_splitk_launch(HR, d.head_units_p[j], kk(k), a, kk(k), w->w_head[j], kk(k),
-                                     &e, reinterpret_cast<float*>(ws + P.splitk), ks, st, fl)
-                : gemm_launch(HR, d.head_units_p[j], kk(k), a, kk(k), w->w_head[j], kk(k), gdt,
+    rc = ks > 1 ? gemm_splitk_launch(HR, d.head_units_p[j], kk(k), a, ka(k), w->w_head[j], kk(k),
+                                     gdt, &e, reinterpret_cast<float*>(ws + P.splitk), ks, st, fl)
+                : gemm_launch(HR, d.head_units_p[j], kk(k), a, ka(k), w->w_head[j], kk(k), gdt,
                               &e, st, fl);
     if (rc) return rc;
     a = head[j & 1];
@@ -803,7 +808,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
     e.bias = w->b_final; e.act = VTD_ACT_NONE;
     e.out = logits; e.ldo = 6; e.out_dtype = VTD_F32;
     e.detections = dets;                              // transform_predictions, fused
-    rc = gemm_launch(HR, 6, kk(k), a, kk(k), w->w_final, kk(k), gdt, &e, st,
+    rc = gemm_launch(HR, 6, kk(k), a, ka(k), w->w_final, kk(k), gdt, &e, st,
                      2.0 * HR * (double)kv * 6);
     if (rc) return rc;
   }
