@@ -184,7 +184,9 @@ int vtd_extract_patches(const float* images_dev, int B, int H, int W, int C, int
  *               (rowadd only for n < rowadd_ncols)) + resid[m][n]
  * for m < M, n < N.  A, Bt in `dtype`; K % VTD_KALIGN == 0; lda, ldb % 8 == 0.
  * dtype VTD_BF16X3: bf16 operands, A the split-bf16 A operand [hi | lo] (lda >= 2 K / 3), Bt
- * the B operand (ldb >= K), K = 3 P with P % 64 == 0 (see "Split-bf16 operands").
+ * the B operand [hi | hi | lo] (ldb >= K; its two hi pieces must be equal, as
+ * vtd_split_bf16x3 role 1 writes them: a kernel may read either), K = 3 P with P % 64 == 0
+ * (see "Split-bf16 operands").
  * out: fp32 (out_dtype 0), bf16 (1) or split-bf16 (VTD_BF16X3: the next GEMM's A operand
  * [hi | lo], two ldo / 2 wide pieces, ldo % 2 == 0, ldo / 2 >= N; bf16 / split-bf16
  * operands only); out2 (nullable) a second bf16 copy.

@@ -95,11 +95,14 @@ def _gemm_x3(L, A32, W32, N=None, **kw):
 
 @pytest.mark.parametrize("M,N,K", [(64, 64, 64), (300, 200, 192), (1024, 768, 768),
                                    (8192, 1024, 256), (512, 17, 256), (300, 512, 192),
-                                   (2048, 2048, 3072), (2176, 2176, 1088)])
+                                   (2048, 2048, 3072), (2176, 2176, 1088), (588, 17, 768),
+                                   (200, 300, 1024)])
 def test_split_gemm_vs_fp64(L, cuda, M, N, K):
     """A split-bf16 GEMM (dtype VTD_BF16X3: bf16 kernels over K' = 3K, A read with the wrap --
     the 256-tile pp2 kernel for the larger shapes, the 128-tile kernel (1024 x 768, 300 x 512)
-    and the skinny kernel for the small ones) against the fp64 product of the f32 operands;
+    and the skinny kernel for the narrow ones, which stages only the [hi | lo] columns of the
+    weights: the head's Dense(17) at K = 768, N = 300 at K = 1024 -- 2048 staged columns, its
+    LDS limit) against the fp64 product of the f32 operands;
     where the forward would split K (vtd_gemm_splitk_choice), the split-K form too, whose
     ranges start before, across and past the wrap (2176 x 2176 x 1088: 4 x 13 K-steps, wrap
     at 34)."""

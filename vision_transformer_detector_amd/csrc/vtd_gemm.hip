@@ -154,7 +154,9 @@ __global__ __launch_bounds__(NT) void gemm_tn_kernel(
 // chunks of SK_CH K-steps, the next chunk's loads in flight while one is multiplied.  These
 // layers are latency-bound: the 128 x 128 kernel ran 17-51 workgroups per layer through
 // dependent register-staged K-steps, the 256-tile kernel needs >= 128 tiles.
-// K % 64 == 0, K <= SK_KMAX.
+// K % 64 == 0, K <= SK_KMAX.  Split-bf16 operands (EpiArgs::aw > 0, K = 3 P): Bt rows are
+// [hi | hi | lo], so only their columns [P, 3P) = [hi | lo] are staged (2 P <= SK_KMAX) and
+// K-step s reads staged step s, or s - P / 32 once past it; A wraps after 2 P.
 constexpr int SK_ROWS = 64, SK_CH = 8, SK_KMAX = 2048;
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(int M, int N, int K,
                                                           const bf16_t* __restrict__ A, int lda,
@@ -181,7 +183,8 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(int M, int N, int K,
   // per chunk: 8-12 serial round trips at the head's K = 544-768); a thread's chunks are
   // 256 apart, stepped as (row, chunk) without a division per chunk.
   {
-    const int kc = K >> 3, nch = 32 * kc;
+    const int bo = e.aw * 32;                     // first staged column (P, or 0)
+    const int kc = (K - bo) >> 3, nch = 32 * kc;
     const int dr = 256 / kc, dc = 256 - dr * kc;
     int r0 = tid / kc, c0 = tid - r0 * kc;
     for (int i0 = tid; i0 < nch; i0 += 8 * 256) {
@@ -193,7 +196,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(int M, int N, int K,
         cc[u] = c0;
         v[u] = i32x4{0, 0, 0, 0};
         if (i0 + u * 256 < nch && n0 + r0 < N)
-          v[u] = *reinterpret_cast<const i32x4*>(Bt + (int64_t)(n0 + r0) * ldb + c0 * 8);
+          v[u] = *reinterpret_cast<const i32x4*>(Bt + (int64_t)(n0 + r0) * ldb + bo + c0 * 8);
         r0 += dr;
         c0 += dc;
         if (c0 >= kc) {
@@ -216,10 +219,11 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(int M, int N, int K,
     for (int j = 0; j < SK_CH; ++j) {
       const int st = s0 + j;
       if (st < nks) {
+        const int sb = st >= e.aw ? st - e.aw : st;   // staged B step (split-bf16 wrap)
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
-          const int r = 16 * cb + fr, c = 4 * (st & 1) + g;
-          const bf16x8 b = *reinterpret_cast<const bf16x8*>(smem + (st >> 1) * 4096 + r * 128 +
+          const int r = 16 * cb + fr, c = 4 * (sb & 1) + g;
+          const bf16x8 b = *reinterpret_cast<const bf16x8*>(smem + (sb >> 1) * 4096 + r * 128 +
                                                             ((c ^ (r & 7)) << 4));
           acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[j]), b,
                                                             acc[cb], 0, 0, 0);
@@ -1991,11 +1995,11 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
              knob(VTD_KNOB_F32_PP2) != 0) {
     f32_pp2_launch(M, N, K, static_cast<const float*>(A), lda, static_cast<const float*>(Bt), ldb,
                    epi, tiles_m, tiles_n, stream);
-  } else if (dtype == VTD_BF16 && K <= SK_KMAX && skinny_choice(M, N, K)) {
+  } else if (dtype == VTD_BF16 && K - 32 * aw <= SK_KMAX && skinny_choice(M, N, K)) {
     EpiArgs e = make_epi_args(epi);
     e.aw = aw;
     const dim3 grid((M + SK_ROWS - 1) / SK_ROWS, (N + 31) / 32);
-    const size_t lds = (size_t)32 * K * 2;
+    const size_t lds = (size_t)32 * (K - 32 * aw) * 2;   // the staged Bt columns
     static std::once_flag once[kMaxDevices];
     once_per_device(once, [] {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_skinny_kernel),
@@ -2038,7 +2042,8 @@ int gemm_splitk_choice(int M, int N, int K, int dtype, int target) {
   const int nk = K / 64;
   if (tiles >= (3 * kSplitTarget) / 4) return 1;
   // a layer the skinny kernel takes (gemm_launch) stays unsplit
-  if (tiles < kMinBigTiles && K <= SK_KMAX && skinny_choice(M, N, K)) return 1;
+  const int k_staged = dtype == VTD_BF16X3 ? 2 * (K / 3) : K;   // the skinny kernel's Bt in LDS
+  if (tiles < kMinBigTiles && k_staged <= SK_KMAX && skinny_choice(M, N, K)) return 1;
   const int s = std::min((kSplitTarget + tiles - 1) / tiles, nk / kSplitMinSteps);
   if (s < 2) return 1;
   const int nks = (nk + s - 1) / s;
