@@ -234,11 +234,11 @@ def _attn_ref(qkv, B, N, H, dk, dkp):
                                       # N = 1600 (5 waves per workgroup), C5's 576 (6), ragged
                                       (2, 1600, 2, 64), (3, 576, 3, 64), (1, 300, 2, 64),
                                       (2, 257, 1, 64), (1, 1100, 1, 48)])
-@pytest.mark.parametrize("variant", [-1, 5, 6, 7, 8])
+@pytest.mark.parametrize("variant", [-1, 5, 6])
 def test_attention(L, cuda, dtype, B, N, H, dk, variant):
     if variant == 5 and (dtype != "bf16" or dk > 64 or not 192 < N <= 256):
         pytest.skip("the variant applies to bf16, dkp 64, N in (192, 256] only")
-    if variant in (6, 7, 8) and (dtype != "bf16" or not 32 < dk <= 64):
+    if variant == 6 and (dtype != "bf16" or not 32 < dk <= 64):
         pytest.skip("the long-sequence kernels apply to bf16, dkp 64 (any N when forced)")
     code, tdt = _dt(L, dtype)
     dkp = 32 if dk <= 32 else (64 if dk <= 64 else 128)

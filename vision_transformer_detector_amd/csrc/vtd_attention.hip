@@ -265,17 +265,12 @@ struct AttnBf16Cfg {
 // XCD-aware (xcd_remap != 0): blocks b, b + 8, ... share an XCD and walk one contiguous range
 // of (pair, query block) ids, so a pair's query blocks run on one XCD and read its K / V
 // through that XCD's L2 once instead of once per XCD from beyond it.
-// QB: query blocks of 32 per wave (2: dkp 64, bf16 output only).  Each K fragment and each
-// V^T tr-read from LDS then feeds QB MFMAs (one per query block): LDS read traffic per score
-// halves at QB = 2, for twice the accumulator registers (<= 256 VGPRs: 2 waves per SIMD).
-template <int DKP, int NWG, bool MX8 = false, int QB = 1>
-__global__ __launch_bounds__(64 * NWG, QB == 2 ? (NWG == 4 ? 2 : 1) : (NWG == 4 ? (DKP == 128 ? 2 : 3) : 2))
-void attention_bf16_kernel(
+template <int DKP, int NWG, bool MX8 = false>
+__global__ __launch_bounds__(64 * NWG, NWG == 4 ? (DKP == 128 ? 2 : 3) : 2) void attention_bf16_kernel(
     const bf16_t* __restrict__ qkv, int N, int heads, int ldqkv, float scale_log2,
     bf16_t* __restrict__ out, int ldo, uint8_t* __restrict__ s8, int64_t s_rows, int nqb,
     int xcd_remap) {
   using C = AttnBf16Cfg<DKP>;
-  static_assert(QB == 1 || (QB == 2 && !MX8 && DKP == 64), "two query blocks: bf16 out, dkp 64");
   typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -290,16 +285,15 @@ void attention_bf16_kernel(
   const int b = pair / heads, h = pair - b * heads;
   const int inner = heads * DKP;
   const int64_t row0 = (int64_t)b * N;
-  const int q0 = (qb * NWG + wave) * 32 * QB;
+  const int q0 = (qb * NWG + wave) * 32;
   const bool active = q0 < N;
 
   // Q pre-scaled by scale * log2(e) (keras scales the query by 1 / sqrt(key_dim) before
   // Q K^T [upstream]; the log2(e) factor makes the scores log2 units) and rounded to bf16
   // again: a score is then exp2'ed as it leaves the MFMA, with no per-score multiply
-  bf16x8 qf[QB][C::KSTEPS];
-#pragma unroll
-  for (int u = 0; u < QB; ++u) {
-    const int q = min(q0 + 32 * u + col, N - 1);
+  bf16x8 qf[C::KSTEPS];
+  {
+    const int q = min(q0 + col, N - 1);
     const bf16_t* qp = qkv + (row0 + q) * ldqkv + h * DKP;
 #pragma unroll
     for (int st = 0; st < C::KSTEPS; ++st) {
@@ -309,16 +303,14 @@ void attention_bf16_kernel(
       for (int j = 0; j < 4; ++j)
         sc[j] = (int)pack_bf16x2(__uint_as_float((uint32_t)raw[j] << 16) * scale_log2,
                                  __uint_as_float((uint32_t)raw[j] & 0xffff0000u) * scale_log2);
-      qf[u][st] = __builtin_bit_cast(bf16x8, sc);
+      qf[st] = __builtin_bit_cast(bf16x8, sc);
     }
   }
-  f32x16 o[QB][C::DB];
+  f32x16 o[C::DB];
 #pragma unroll
-  for (int u = 0; u < QB; ++u)
+  for (int i = 0; i < C::DB; ++i)
 #pragma unroll
-    for (int i = 0; i < C::DB; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[u][i][r] = 0.f;
+    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
   // Running max m_run (log2 units, kept exactly representable in bf16) subtracted INSIDE the
   // score MFMA chain: one extra K-step multiplies the constant A column e_0 (1 at k = 0) by the
   // B column -m_run (k = 0), so each score leaves the matrix core as s - m_run and P is one
@@ -326,19 +318,13 @@ void attention_bf16_kernel(
   // SUMMFMA: the row sum l rides in the PV MFMAs as a 32-row block of ones in V^T (every row
   // of osum = sum_k P[k][q] of the bf16 P actually used), instead of one VALU add per score;
   // otherwise l_run sums the fp32 P.  Both only where the registers allow it: the 4-wave
-  // one-block workgroups (3 per CU; dkp <= 64 for SUMMFMA).  The 8-wave ones (C5's MX-fp8
-  // epilogue, 2 workgroups per CU at <= 128 VGPRs) and the two-block waves keep the running
-  // max outside the MFMA chain (OFFM false: P = exp2(s - m_run), m_run from -inf) -- with both
-  // tricks the 8-wave kernel took 141 VGPRs, one workgroup per CU: C5 fp8 attention
-  // 261 -> 345 us (profiles/r06_s1_*).
-  constexpr bool OFFM = NWG == 4 && QB == 1;
+  // workgroups (3 per CU; dkp <= 64 for SUMMFMA).  The 8-wave ones (C5's MX-fp8 epilogue,
+  // 2 workgroups per CU at <= 128 VGPRs) keep the running max outside the MFMA chain
+  // (OFFM false: P = exp2(s - m_run), m_run from -inf) -- with both tricks they took 141
+  // VGPRs, one workgroup per CU: C5 fp8 attention 261 -> 345 us (profiles/r06_s1_*).
+  constexpr bool OFFM = NWG == 4;
   constexpr bool SUMMFMA = OFFM && DKP <= 64;
-  float m_run[QB], l_run[QB];
-#pragma unroll
-  for (int u = 0; u < QB; ++u) {
-    m_run[u] = OFFM ? 0.f : -INFINITY;
-    l_run[u] = 0.f;
-  }
+  float m_run = OFFM ? 0.f : -INFINITY, l_run = 0.f;
   const bf16_t one_bf16 = 0x3F80;
   const bf16x8 a_e0 = {(short)(half == 0 ? one_bf16 : 0), 0, 0, 0, 0, 0, 0, 0};
   const bf16x8 a_ones = {(short)one_bf16, (short)one_bf16, (short)one_bf16, (short)one_bf16,
@@ -400,126 +386,113 @@ void attention_bf16_kernel(
       // ragged: N = 196 leaves 4 keys in it, one block)
       const int nkb = LAST ? min(2, (N - kv0 + 31) >> 5) : 2;
       const bool ragged = LAST && kv0 + C::KC > N;
-      f32x16 s[QB][2];
+      f32x16 s[2];
       const f32x16 zero = {};
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         if (kb < nkb) {
           const char* krow = kl + (kb * 32 + col) * C::KS;
+          if constexpr (OFFM) s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_e0, b_m, zero, 0, 0, 0);   // -m_run
+          else s[kb] = zero;
 #pragma unroll
-          for (int u = 0; u < QB; ++u) {
-            if constexpr (OFFM) s[u][kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_e0, b_m, zero, 0, 0, 0);   // -m_run
-            else s[u][kb] = zero;
-          }
-#pragma unroll
-          for (int st = 0; st < C::KSTEPS; ++st) {
-            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(krow + (st * 16 + half * 8) * 2);
-#pragma unroll
-            for (int u = 0; u < QB; ++u)
-              s[u][kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[u][st], s[u][kb], 0, 0, 0);
-          }
+          for (int st = 0; st < C::KSTEPS; ++st)
+            s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                *reinterpret_cast<const bf16x8*>(krow + (st * 16 + half * 8) * 2), qf[st],
+                s[kb], 0, 0, 0);
         }
       }
       // scores beyond N (ragged last chunk only) are -inf
       if (ragged) {
 #pragma unroll
-        for (int u = 0; u < QB; ++u)
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kv0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+            if (key >= N) s[kb][r] = -INFINITY;
+          }
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+        if (kb < nkb) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
+        }
+      mx = pair_max(mx);              // (relative to m_run) lane l ^ 32 holds the other keys
+      // deferred rescale: the accumulators are rescaled only when some lane's max grows by
+      // more than 8 (log2 units), so exp2 arguments stay <= 8 + 1/8 (P <= 2^8.125, exact in the
+      // bf16 P operand's range, l and O in fp32); the final 1/l normalises whatever max was
+      // used consistently for O and l.  The first chunk always sets the max.
+      if constexpr (OFFM) {
+        if (__builtin_amdgcn_ballot_w64(c == 0 || mx > 8.f)) {
+          const float m_new = bf16_round(m_run + (c == 0 ? mx : fmaxf(mx, 0.f)));
+          const float dlt = m_new - m_run;
+          // (first chunk: O and l are still 0; dlt may be any size there)
+          const float alpha = c == 0 ? 0.f : __builtin_amdgcn_exp2f(-dlt);
+          m_run = m_new;
+          b_m[0] = (short)(half == 0 ? f32_to_bf16(-m_new) : 0);
+          l_run *= alpha;
+          osum[0] *= alpha;
+#pragma unroll
+          for (int i = 0; i < C::DB; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
 #pragma unroll
           for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int key = kv0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-              if (key >= N) s[u][kb][r] = -INFINITY;
-            }
-      }
-#pragma unroll
-      for (int u = 0; u < QB; ++u) {
-        float mx = -INFINITY;
+            for (int r = 0; r < 16; ++r) s[kb][r] -= dlt;
+        }
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
           if (kb < nkb) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[u][kb][r]);
+            for (int r = 0; r < 16; ++r) s[kb][r] = __builtin_amdgcn_exp2f(s[kb][r]);
           }
-        mx = pair_max(mx);            // (relative to m_run) lane l ^ 32 holds the other keys
-        // deferred rescale: the accumulators are rescaled only when some lane's max grows by
-        // more than 8 (log2 units), so exp2 arguments stay <= 8 + 1/8 (P <= 2^8.125, exact in the
-        // bf16 P operand's range, l and O in fp32); the final 1/l normalises whatever max was
-        // used consistently for O and l.  The first chunk always sets the max.
-        if constexpr (OFFM) {
-          if (__builtin_amdgcn_ballot_w64(c == 0 || mx > 8.f)) {
-            const float m_new = bf16_round(m_run[u] + (c == 0 ? mx : fmaxf(mx, 0.f)));
-            const float dlt = m_new - m_run[u];
-            // (first chunk: O and l are still 0; dlt may be any size there)
-            const float alpha = c == 0 ? 0.f : __builtin_amdgcn_exp2f(-dlt);
-            m_run[u] = m_new;
-            b_m[0] = (short)(half == 0 ? f32_to_bf16(-m_new) : 0);
-            l_run[u] *= alpha;
-            osum[0] *= alpha;
+      } else {
+        // (absolute scores) rescale only when some lane's max grows by more than 8
+        if (__builtin_amdgcn_ballot_w64(mx > m_run + 8.f)) {
+          const float m_new = fmaxf(m_run, mx);
+          const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+          m_run = m_new;
+          l_run *= alpha;
 #pragma unroll
-            for (int i = 0; i < C::DB; ++i)
+          for (int i = 0; i < C::DB; ++i)
 #pragma unroll
-              for (int r = 0; r < 16; ++r) o[u][i][r] *= alpha;
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-              for (int r = 0; r < 16; ++r) s[u][kb][r] -= dlt;
-          }
-#pragma unroll
-          for (int kb = 0; kb < 2; ++kb)
-            if (kb < nkb) {
-#pragma unroll
-              for (int r = 0; r < 16; ++r) s[u][kb][r] = __builtin_amdgcn_exp2f(s[u][kb][r]);
-            }
-        } else {
-          // (absolute scores) rescale only when some lane's max grows by more than 8
-          if (__builtin_amdgcn_ballot_w64(mx > m_run[u] + 8.f)) {
-            const float m_new = fmaxf(m_run[u], mx);
-            const float alpha = __builtin_amdgcn_exp2f(m_run[u] - m_new);
-            m_run[u] = m_new;
-            l_run[u] *= alpha;
-#pragma unroll
-            for (int i = 0; i < C::DB; ++i)
-#pragma unroll
-              for (int r = 0; r < 16; ++r) o[u][i][r] *= alpha;
-          }
-          const float nm = -m_run[u];
-#pragma unroll
-          for (int kb = 0; kb < 2; ++kb)
-            if (kb < nkb) {
-#pragma unroll
-              for (int r = 0; r < 16; ++r) s[u][kb][r] = __builtin_amdgcn_exp2f(s[u][kb][r] + nm);
-            }
+            for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
         }
-        if constexpr (!SUMMFMA) {
-          // scalar fp32 adds (the file is built without SLP packing: packed f32 ops cost more
-          // issue cycles beside MFMAs than two scalar ones); even / odd scores summed apart
-          float ps0 = 0.f, ps1 = 0.f;
+        const float nm = -m_run;
 #pragma unroll
-          for (int kb = 0; kb < 2; ++kb)
-            if (kb < nkb) {
+        for (int kb = 0; kb < 2; ++kb)
+          if (kb < nkb) {
 #pragma unroll
-              for (int r = 0; r < 16; r += 2) {
-                ps0 += s[u][kb][r];
-                ps1 += s[u][kb][r + 1];
-              }
+            for (int r = 0; r < 16; ++r) s[kb][r] = __builtin_amdgcn_exp2f(s[kb][r] + nm);
+          }
+      }
+      if constexpr (!SUMMFMA) {
+        // scalar fp32 adds (the file is built without SLP packing: packed f32 ops cost more
+        // issue cycles beside MFMAs than two scalar ones); even / odd scores summed apart
+        float ps0 = 0.f, ps1 = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+          if (kb < nkb) {
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+              ps0 += s[kb][r];
+              ps1 += s[kb][r + 1];
             }
-          l_run[u] += ps0 + ps1;
-        }
+          }
+        l_run += ps0 + ps1;
       }
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
         if (kb < nkb) {
 #pragma unroll
           for (int st = 0; st < 2; ++st) {
-            bf16x8 pb[QB];
-#pragma unroll
-            for (int u = 0; u < QB; ++u)
-              pb[u] = __builtin_bit_cast(
-                  bf16x8, i32x4{(int)pack_bf16x2(s[u][kb][8 * st + 0], s[u][kb][8 * st + 1]),
-                                (int)pack_bf16x2(s[u][kb][8 * st + 2], s[u][kb][8 * st + 3]),
-                                (int)pack_bf16x2(s[u][kb][8 * st + 4], s[u][kb][8 * st + 5]),
-                                (int)pack_bf16x2(s[u][kb][8 * st + 6], s[u][kb][8 * st + 7])});
+            const bf16x8 pb = __builtin_bit_cast(
+                bf16x8, i32x4{(int)pack_bf16x2(s[kb][8 * st + 0], s[kb][8 * st + 1]),
+                              (int)pack_bf16x2(s[kb][8 * st + 2], s[kb][8 * st + 3]),
+                              (int)pack_bf16x2(s[kb][8 * st + 4], s[kb][8 * st + 5]),
+                              (int)pack_bf16x2(s[kb][8 * st + 6], s[kb][8 * st + 7])});
             const int key0 = kb * 32 + 16 * st + tr_key;
 #pragma unroll
             for (int db = 0; db < C::DB; ++db) {
@@ -528,11 +501,9 @@ void attention_bf16_kernel(
               const bf16x4 hi =
                   __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(va + 8 * C::VS));
               const bf16x8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-              for (int u = 0; u < QB; ++u)
-                o[u][db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb[u], o[u][db], 0, 0, 0);
+              o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, pb, o[db], 0, 0, 0);
             }
-            if constexpr (SUMMFMA) osum = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_ones, pb[0], osum, 0, 0, 0);
+            if constexpr (SUMMFMA) osum = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_ones, pb, osum, 0, 0, 0);
           }
         }
     }
@@ -542,6 +513,9 @@ void attention_bf16_kernel(
   for (int c = 0; c + 1 < nchunks; ++c) chunk(c, std::false_type{});
   chunk(nchunks - 1, std::true_type{});
   if (!active) return;
+  // osum rows hold the whole key sum (both lane halves' keys); l_run holds this half's
+  const float inv = 1.f / (SUMMFMA ? osum[0] : pair_sum(l_run));
+  const int q = q0 + col;
   if constexpr (!MX8 && DKP == 64) {
     // bf16 output through LDS (free after the loop's last barrier): a lane holds 16-B
     // pieces of one query row spread over 8 columns groups, so direct stores write 16 B
@@ -549,33 +523,22 @@ void attention_bf16_kernel(
     // 8-B writes hit distinct banks) every store instruction writes 8 whole 128-B rows.
     char* wst = smem + wave * (32 * 144);
 #pragma unroll
-    for (int u = 0; u < QB; ++u) {
-      // osum rows hold the whole key sum (both lane halves' keys); l_run holds this half's
-      const float inv = 1.f / (SUMMFMA ? osum[0] : pair_sum(l_run[u]));
-      const int qu = q0 + 32 * u;
+    for (int db = 0; db < C::DB; ++db)
 #pragma unroll
-      for (int db = 0; db < C::DB; ++db)
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<uint2*>(wst + col * 144 + (db * 32 + 8 * g + 4 * half) * 2) =
+            uint2{pack_bf16x2(o[db][4 * g + 0] * inv, o[db][4 * g + 1] * inv),
+                  pack_bf16x2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv)};
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // wave-local: own writes landed
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<uint2*>(wst + col * 144 + (db * 32 + 8 * g + 4 * half) * 2) =
-              uint2{pack_bf16x2(o[u][db][4 * g + 0] * inv, o[u][db][4 * g + 1] * inv),
-                    pack_bf16x2(o[u][db][4 * g + 2] * inv, o[u][db][4 * g + 3] * inv)};
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // wave-local: own writes landed
-#pragma unroll
-      for (int pass = 0; pass < 4; ++pass) {
-        const int r = pass * 8 + (lane >> 3), ch = lane & 7;
-        if (qu + r < N)
-          *reinterpret_cast<i32x4*>(out + (row0 + qu + r) * ldo + h * DKP + ch * 8) =
-              *reinterpret_cast<const i32x4*>(wst + r * 144 + ch * 16);
-      }
-      // the next block's restage writes follow this block's reads (in order per wave)
-      if constexpr (QB > 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int pass = 0; pass < 4; ++pass) {
+      const int r = pass * 8 + (lane >> 3), ch = lane & 7;
+      if (q0 + r < N)
+        *reinterpret_cast<i32x4*>(out + (row0 + q0 + r) * ldo + h * DKP + ch * 8) =
+            *reinterpret_cast<const i32x4*>(wst + r * 144 + ch * 16);
     }
     return;
   }
-  // osum rows hold the whole key sum (both lane halves' keys); l_run holds this half's
-  const float inv = 1.f / (SUMMFMA ? osum[0] : pair_sum(l_run[0]));
-  const int q = q0 + col;
   if (q >= N) return;          // lanes l and l ^ 32 hold the same query: both leave or stay
   if constexpr (MX8) {
     uint8_t* qp = reinterpret_cast<uint8_t*>(out) + (row0 + q) * (int64_t)ldo + h * DKP;
@@ -585,7 +548,7 @@ void attention_bf16_kernel(
       float amax = 0.f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        v[i] = bf16_round(o[0][db][i] * inv);
+        v[i] = bf16_round(o[db][i] * inv);
         amax = fmaxf(amax, fabsf(v[i]));
       }
       amax = pair_max(amax);
@@ -608,8 +571,8 @@ void attention_bf16_kernel(
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int d = db * 32 + 8 * g + 4 * half;
-      const uint2 v = {pack_bf16x2(o[0][db][4 * g + 0] * inv, o[0][db][4 * g + 1] * inv),
-                       pack_bf16x2(o[0][db][4 * g + 2] * inv, o[0][db][4 * g + 3] * inv)};
+      const uint2 v = {pack_bf16x2(o[db][4 * g + 0] * inv, o[db][4 * g + 1] * inv),
+                       pack_bf16x2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv)};
       *reinterpret_cast<uint2*>(op + d) = v;
     }
 }
@@ -1720,25 +1683,25 @@ int launch_x3(const void* qkv, int B, int N, int heads, int ldqkv, float scale, 
   return VTD_OK;
 }
 
-template <int DKP, int NWG, bool MX8 = false, int QB = 1>
+template <int DKP, int NWG, bool MX8 = false>
 int launch_bf16_v2(const void* qkv, int B, int N, int heads, int ldqkv, float scale,
                    void* out, int ldo, hipStream_t stream, uint8_t* s8 = nullptr,
                    int64_t s_rows = 0) {
   using C = AttnBf16Cfg<DKP>;
-  const int nq = (N + 31) / 32, nqb = (nq + NWG * QB - 1) / (NWG * QB);
+  const int nq = (N + 31) / 32, nqb = (nq + NWG - 1) / NWG;
   VTD_CHECK_ARG((int64_t)nqb * heads * B < INT32_MAX, "attention: grid too large");
   const dim3 grid(nqb * heads * B);
   static std::once_flag once[kMaxDevices];
   once_per_device(once, [] {
     (void)hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&attention_bf16_kernel<DKP, NWG, MX8, QB>),
+        reinterpret_cast<const void*>(&attention_bf16_kernel<DKP, NWG, MX8>),
         hipFuncAttributeMaxDynamicSharedMemorySize, 2 * C::BUF);
   });
   // XCD-aware order: C3 attention 382.5-383.2 vs 384.0-384.2 us per launch, forward
   // 1,812-1,813 vs 1,783-1,790 img/s (profiles/r03_attn_xcd_order_ab.log); the kernel is
   // VALU-bound, its K / V re-reads were mostly served beyond L2 at no visible cost
   const int xcd_remap = 1;
-  hipLaunchKernelGGL((attention_bf16_kernel<DKP, NWG, MX8, QB>), grid, dim3(64 * NWG), 2 * C::BUF,
+  hipLaunchKernelGGL((attention_bf16_kernel<DKP, NWG, MX8>), grid, dim3(64 * NWG), 2 * C::BUF,
                      stream, static_cast<const bf16_t*>(qkv), N, heads, ldqkv,
                      scale * 1.4426950408889634f, static_cast<bf16_t*>(out), ldo, s8, s_rows,
                      nqb, xcd_remap);
@@ -1810,11 +1773,6 @@ int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqk
     // streaming kernel at C3 / C5, profiles/r05_attn_fl_ab.log)
     if (dkp == 64 && ldqkv % 8 == 0 && ldo % 8 == 0 && v1 == 6)
       return launch_bf16_fl(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
-    // 7 / 8: two 32-query blocks per wave (dkp 64) in 4- / 8-wave workgroups
-    if (dkp == 64 && v1 == 7)
-      return launch_bf16_v2<64, 4, false, 2>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
-    if (dkp == 64 && v1 == 8)
-      return launch_bf16_v2<64, 8, false, 2>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
     if (v1 == 1) {
       if (dkp == 32) return launch<bf16_t, 32>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
       if (dkp == 64) return launch<bf16_t, 64>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
