@@ -609,6 +609,12 @@ def main():
         "rank_ms_min": round(1e3 * spread["min_s"] / args.steps, 3),
         "rank_ms_max": round(1e3 * spread["max_s"] / args.steps, 3),
     }
+    if args.dtype == "bf16x3":
+        # the split-bf16 mode runs each algorithmic FLOP as three bf16 MFMA products: the
+        # matrix cores' load is 3x the algorithmic utilisation above
+        out["mfma_util_hw"] = round(3 * out["mfma_util_attn_mlp"], 4)
+        out["roofline"]["frac_hw"] = (round(3 * out["roofline"]["frac"], 4)
+                                      if out["roofline"]["frac"] else None)
     if world == 1 and headline and not args.no_parity_mode:
         out["parity_mode"] = parity_mode(args, dev, kw)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
