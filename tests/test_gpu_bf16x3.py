@@ -273,7 +273,8 @@ def _attn_ref64(qkv, B, N, H, dk, dkp):
 @pytest.mark.parametrize("B,N,H,dk", [(2, 196, 3, 64), (1, 70, 2, 40), (1, 1, 1, 32),
                                       (1, 333, 2, 128), (2, 1600, 2, 64), (3, 576, 3, 64),
                                       (40, 196, 12, 64), (1, 64, 4, 20), (1, 129, 2, 100)])
-def test_attention_split_vs_fp64(L, cuda, B, N, H, dk):
+@pytest.mark.parametrize("variant", [-1, 10])
+def test_attention_split_vs_fp64(L, cuda, B, N, H, dk, variant):
     """vtd_attention with dtype VTD_BF16X3 (vtd.py:364-369 in the split-bf16 parity mode): f32
     query / key / value in, every product as hi.hi + lo.hi + hi.lo on the bf16 MFMA with fp32
     softmax statistics, the output written as the attention-output Dense's split-bf16 A operand
@@ -290,8 +291,11 @@ def test_attention_split_vs_fp64(L, cuda, B, N, H, dk):
     P = H * dkp + 64
     out = torch.full((B * N, 2 * P), -1, dtype=torch.int16, device=cuda)
     qkv_d = torch.from_numpy(qkv).to(cuda)
-    L.check(L.lib.vtd_attention(qkv_d.data_ptr(), B, N, H, dkp, ld, 1.0 / math.sqrt(dk),
-                                out.data_ptr(), 2 * P, L.BF16X3, L.stream_ptr()), "attention")
+    if variant == 10 and dkp != 64:
+        pytest.skip("knob 10 (64-key chunks, one workgroup per CU) is a dkp-64 variant")
+    with L.knob(L.KNOB_ATTN_VARIANT, variant):
+        L.check(L.lib.vtd_attention(qkv_d.data_ptr(), B, N, H, dkp, ld, 1.0 / math.sqrt(dk),
+                                    out.data_ptr(), 2 * P, L.BF16X3, L.stream_ptr()), "attention")
     torch.cuda.synchronize()
     got = as_u16(out)
     inner = H * dkp

@@ -1408,9 +1408,10 @@ int launch_bf16_fl(const void* qkv, int B, int N, int heads, int ldqkv, float sc
 // planes with the bf16 kernel's row strides, so the K reads and the V^T tr-reads are the
 // bf16 kernel's).  The output is written directly as the attention_output GEMM's split-bf16
 // A operand [hi | lo] (two P = ldo / 2 wide pieces), so no split pass follows it.
-template <int DKP>
+template <int DKP, int KC_ = 64>
 struct AttnX3Cfg {
-  static constexpr int KC = 64;                       // keys per chunk
+  static constexpr int KC = KC_;                      // keys per chunk
+  static constexpr int NKB = KC / 32;                 // 32-key blocks per chunk
   static constexpr int KS = DKP * 2 + 16;             // K row stride (bytes, per plane)
   static constexpr int VS = DKP * 2 + 64;             // V row stride (bytes, per plane)
   static constexpr int PLANE = KC * KS + KC * VS;     // K then V image of one plane
@@ -1432,11 +1433,11 @@ __device__ __forceinline__ void split8(const f32x4& a, const f32x4& b, bf16x8& h
                                         (int)pack_lo_bf16x2(b[2], b[3], h3)});
 }
 
-template <int DKP, int NWG>
-__global__ __launch_bounds__(64 * NWG, 1) void attention_x3_kernel(
+template <int DKP, int NWG, int KC = 64, int MINB = 1>
+__global__ __launch_bounds__(64 * NWG, MINB) void attention_x3_kernel(
     const float* __restrict__ qkv, int N, int heads, int ldqkv, float scale_log2,
     bf16_t* __restrict__ out, int ldo, int nqb) {
-  using C = AttnX3Cfg<DKP>;
+  using C = AttnX3Cfg<DKP, KC>;
   typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -1519,11 +1520,11 @@ __global__ __launch_bounds__(64 * NWG, 1) void attention_x3_kernel(
     if (active) {
       const char* kl = smem + (c & 1) * C::BUF;      // hi plane; lo plane at + PLANE
       const char* vl = kl + C::KC * C::KS;
-      const int nkb = LAST ? min(2, (N - kv0 + 31) >> 5) : 2;
+      const int nkb = LAST ? min(C::NKB, (N - kv0 + 31) >> 5) : C::NKB;
       const bool ragged = LAST && kv0 + C::KC > N;
-      f32x16 s[2];
+      f32x16 s[C::NKB];
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
+      for (int kb = 0; kb < C::NKB; ++kb) {
         if (kb < nkb) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
@@ -1541,7 +1542,7 @@ __global__ __launch_bounds__(64 * NWG, 1) void attention_x3_kernel(
       }
       if (ragged) {
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
+        for (int kb = 0; kb < C::NKB; ++kb)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int key = kv0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
@@ -1550,7 +1551,7 @@ __global__ __launch_bounds__(64 * NWG, 1) void attention_x3_kernel(
       }
       float mx = -INFINITY;
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < C::NKB; ++kb)
         if (kb < nkb) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kb][r]);
@@ -1570,7 +1571,7 @@ __global__ __launch_bounds__(64 * NWG, 1) void attention_x3_kernel(
       float ps0 = 0.f, ps1 = 0.f;
       const float nm = -m_run;
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < C::NKB; ++kb)
         if (kb < nkb) {
 #pragma unroll
           for (int r = 0; r < 16; r += 2) {
@@ -1584,7 +1585,7 @@ __global__ __launch_bounds__(64 * NWG, 1) void attention_x3_kernel(
         }
       l_run += ps0 + ps1;
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < C::NKB; ++kb)
         if (kb < nkb) {
 #pragma unroll
           for (int st = 0; st < 2; ++st) {
@@ -1664,20 +1665,23 @@ __global__ __launch_bounds__(64 * NWG, 1) void attention_x3_kernel(
     }
 }
 
-template <int DKP>
+template <int DKP, int KC = 64, int MINB = 1>
 int launch_x3(const void* qkv, int B, int N, int heads, int ldqkv, float scale, void* out,
               int ldo, hipStream_t stream) {
-  using C = AttnX3Cfg<DKP>;
+  using C = AttnX3Cfg<DKP, KC>;
   constexpr int NWG = 8;
+  // the K / V double buffer, or (dkp 64) the output restage: a hi and a lo image of 32 rows
+  // x 144 B per wave
+  constexpr int LDS = std::max(2 * C::BUF, DKP == 64 ? NWG * 2 * 32 * 144 : 0);
   const int nq = (N + 31) / 32, nqb = (nq + NWG - 1) / NWG;
   VTD_CHECK_ARG((int64_t)nqb * heads * B < INT32_MAX, "attention: grid too large");
   static std::once_flag once[kMaxDevices];
   once_per_device(once, [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_x3_kernel<DKP, NWG>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 2 * C::BUF);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_x3_kernel<DKP, NWG, KC, MINB>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
   });
-  hipLaunchKernelGGL((attention_x3_kernel<DKP, NWG>), dim3(nqb * heads * B), dim3(64 * NWG),
-                     2 * C::BUF, stream, static_cast<const float*>(qkv), N, heads, ldqkv,
+  hipLaunchKernelGGL((attention_x3_kernel<DKP, NWG, KC, MINB>), dim3(nqb * heads * B),
+                     dim3(64 * NWG), LDS, stream, static_cast<const float*>(qkv), N, heads, ldqkv,
                      scale * 1.4426950408889634f, static_cast<bf16_t*>(out), ldo, nqb);
   VTD_LAUNCH_CHECK("attention_x3");
   return VTD_OK;
@@ -1750,6 +1754,12 @@ int attention_launch(const void* qkv, int B, int N, int heads, int dkp, int ldqk
                flops > 0 ? flops : 4.0 * B * heads * (double)N * N * dkp);
   if (dtype == VTD_BF16X3) {
     if (dkp == 32) return launch_x3<32>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
+    // dkp 64: 32-key chunks at <= 128 VGPRs, two workgroups per CU (the output restage's
+    // 72 KiB of LDS each): C2 attention 208 -> 158 us per layer, bf16x3 forward +1.4 %, C3
+    // 769 -> 713 us (profiles/r06_x3_attn_kc32_ab.log); knob VTD_KNOB_ATTN_VARIANT 10: the
+    // 64-key chunks at one workgroup per CU (169 VGPRs, 84 KiB)
+    if (dkp == 64 && knob(VTD_KNOB_ATTN_VARIANT) != 10)
+      return launch_x3<64, 32, 2>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
     if (dkp == 64) return launch_x3<64>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
     return launch_x3<128>(qkv, B, N, heads, ldqkv, scale, out, ldo, stream);
   }
