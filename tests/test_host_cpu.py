@@ -187,6 +187,18 @@ def test_invalid_op_args_raise_before_any_launch(L):
         L.check(L.lib.vtd_attention(None, 1, 4, 1, 48, 144, 1.0, None, 48, L.BF16, None))
     with pytest.raises(ValueError):
         L.check(L.lib.vtd_layernorm(None, L.F32, 1, 4, 4, None, None, 1e-3, None, 4, L.F32, None))
+    # split-bf16 A operand (dtype VTD_BF16X3): K = 3 P with P % 64 == 0, lda >= 2 P
+    e.out, e.ldo, e.out_dtype = 1, 16, L.F32
+    for K, lda in ((128, 128), (192, 120), (576, 256)):
+        with pytest.raises(ValueError):
+            L.check(L.lib.vtd_gemm(16, 16, K, 1, lda, 1, K, L.BF16X3, ctypes.byref(e), None))
+        with pytest.raises(ValueError):
+            L.check(L.lib.vtd_gemm_splitk(16, 16, K, 1, lda, 1, K, L.BF16X3, ctypes.byref(e), 16,
+                                          1 << 20, 2, None))
+    # a split-bf16 output: two ldo / 2 wide pieces
+    e.ldo, e.out_dtype = 33, L.BF16X3
+    with pytest.raises(ValueError):
+        L.check(L.lib.vtd_gemm(16, 16, 64, 1, 64, 1, 64, L.BF16, ctypes.byref(e), None))
 
 
 def test_presets_param_counts():
