@@ -210,8 +210,8 @@ typedef struct vtd_epilogue {
    * and 64-column block b, statout[2 (b stat_ld + m)] = mean and [.. + 1] = sum of squared
    * deviations from that mean, of the block's 64 stored bf16 values (centred partials:
    * exact whatever |mean| / std).  Slot-major: one plane of stat_ld >= M rows per block.
-   * Only on full 256 x 256 tiles of the bf16 fast epilogues -- M % 256 == N % 256 == 0 and
-   * at least 64 tiles (else vtd_gemm returns VTD_ERR_UNSUPPORTED); NULL: none. */
+   * Only on full 256 x 256 tiles of the bf16 fast epilogues -- dtype VTD_BF16, M % 256 ==
+   * N % 256 == 0 and at least 64 tiles (else vtd_gemm returns VTD_ERR_UNSUPPORTED); NULL: none. */
   float* statout; int stat_ld;
   /* out_dtype VTD_FP8 (vtd_gemm_mx8 only, every tile full: M % 256 == N % 256 == 0): the
    * output is written as the next GEMM's MX-fp8 A operand, byte for byte what

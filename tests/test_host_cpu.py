@@ -195,6 +195,12 @@ def test_invalid_op_args_raise_before_any_launch(L):
         with pytest.raises(ValueError):
             L.check(L.lib.vtd_gemm_splitk(16, 16, K, 1, lda, 1, K, L.BF16X3, ctypes.byref(e), 16,
                                           1 << 20, 2, None))
+    # partial LayerNorm statistics need bf16 operands: refused for a split-bf16 A operand
+    st = L.VtdEpilogue()
+    st.bias, st.out, st.ldo, st.out_dtype = 16, 16, 256, L.BF16
+    st.statout, st.stat_ld = 16, 16384
+    assert L.lib.vtd_gemm(16384, 256, 768, 16, 512, 16, 768, L.BF16X3, ctypes.byref(st),
+                          None) == -2
     # a split-bf16 output: two ldo / 2 wide pieces
     e.ldo, e.out_dtype = 33, L.BF16X3
     with pytest.raises(ValueError):

@@ -1890,9 +1890,10 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
   VTD_CHECK_ARG(!epi->detections || (N == 6 && epi->out_dtype == VTD_F32 &&
                                       epi->scatter_tokens <= 0),
                 "gemm: detections (fused transform_predictions) need N == 6 and an fp32 output");
-  if (epi->statout && !gemm_emits_stats(M, N, dtype, epi))
+  // (a split-bf16 A operand runs the wrap-capable codes only, none of which writes statistics)
+  if (epi->statout && (split_a || !gemm_emits_stats(M, N, dtype, epi)))
     return fail(VTD_ERR_UNSUPPORTED, "gemm: statout needs full 256 x 256 tiles on the bf16 "
-                                     "fast epilogues (see gemm_emits_stats)");
+                                     "fast epilogues and bf16 operands (see gemm_emits_stats)");
   if (lnpart) {
     const int rc = ln_stats_finalize_launch(lnpart, M, lnslots, lnD, lneps,
                                             const_cast<float*>(epi->lnstat), stream);
