@@ -653,10 +653,11 @@ __global__ __launch_bounds__(256) void patches_kernel(
   }
 }
 
-// Unpadded case (H, W multiples of p; p*C % 8 == 0; ld_out == P), bf16 out: a patch row
-// kh of token m is p*C consecutive floats of image row gy*p + kh, so each thread moves 8
-// consecutive floats (two 16-B loads) to one 16-B store with no index arithmetic per
-// element.  Same output as patches_kernel.
+// Unpadded case (H, W multiples of p; p*C % 8 == 0), bf16 out with ld_out == P, or (X3) the
+// split-bf16 operand with ld_out == 2 P: a patch row kh of token m is p*C consecutive floats
+// of image row gy*p + kh, so each thread moves 8 consecutive floats (two 16-B loads) to one
+// 16-B store per piece with no index arithmetic per element.  Same output as patches_kernel.
+template <bool X3 = false>
 __global__ __launch_bounds__(256) void patches_dense_kernel(
     const float* __restrict__ img, int64_t total, int H, int W, int C, int p, int gw, int N,
     bf16_t* __restrict__ out) {
@@ -674,7 +675,13 @@ __global__ __launch_bounds__(256) void patches_dense_kernel(
     const f32x4 v1 = *reinterpret_cast<const f32x4*>(src + 4);
     const uint4 o = {pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3]),
                      pack_bf16x2(v1[0], v1[1]), pack_bf16x2(v1[2], v1[3])};
-    *reinterpret_cast<uint4*>(out + m * (int64_t)(p * p * C) + kh * p * C + c8 * 8) = o;
+    const int P = p * p * C;
+    bf16_t* const op = out + m * (int64_t)(X3 ? 2 * P : P) + kh * p * C + c8 * 8;
+    *reinterpret_cast<uint4*>(op) = o;
+    if constexpr (X3)
+      *reinterpret_cast<uint4*>(op + P) =
+          uint4{pack_lo_bf16x2(v0[0], v0[1], o.x), pack_lo_bf16x2(v0[2], v0[3], o.y),
+                pack_lo_bf16x2(v1[0], v1[1], o.z), pack_lo_bf16x2(v1[2], v1[3], o.w)};
   }
 }
 
@@ -936,13 +943,18 @@ int patches_launch(const float* img, int B, int H, int W, int C, int p, void* ou
   const int64_t total = (int64_t)B * N * ((dtype == VTD_BF16X3 ? ldo / 2 : ldo) / 8);
   const int grid = (int)std::min<int64_t>((total + 255) / 256, 8192);
   ProfScope ps(st, PROF_PATCH, 0.0);
-  if (dtype == VTD_BF16 && pad_h == 0 && pad_w == 0 && (p * C) % 8 == 0 && ldo == P &&
-      (W * C) % 4 == 0 && reinterpret_cast<uintptr_t>(img) % 16 == 0 &&
-      reinterpret_cast<uintptr_t>(out) % 16 == 0) {
+  const bool dense = pad_h == 0 && pad_w == 0 && (p * C) % 8 == 0 && (W * C) % 4 == 0 &&
+                     reinterpret_cast<uintptr_t>(img) % 16 == 0 &&
+                     reinterpret_cast<uintptr_t>(out) % 16 == 0;
+  if (dense && ((dtype == VTD_BF16 && ldo == P) || (dtype == VTD_BF16X3 && ldo == 2 * P))) {
     const int64_t tot = (int64_t)B * N * P / 8;
     const int gd = (int)std::min<int64_t>((tot + 255) / 256, 16384);
-    hipLaunchKernelGGL(patches_dense_kernel, dim3(gd), dim3(256), 0, st, img, tot, H, W, C, p,
-                       gw, N, static_cast<bf16_t*>(out));
+    if (dtype == VTD_BF16X3)
+      hipLaunchKernelGGL(patches_dense_kernel<true>, dim3(gd), dim3(256), 0, st, img, tot, H, W,
+                         C, p, gw, N, static_cast<bf16_t*>(out));
+    else
+      hipLaunchKernelGGL(patches_dense_kernel<false>, dim3(gd), dim3(256), 0, st, img, tot, H, W,
+                         C, p, gw, N, static_cast<bf16_t*>(out));
   } else if (dtype == VTD_BF16X3)
     hipLaunchKernelGGL((patches_kernel<bf16_t, true>), dim3(grid), dim3(256), 0, st, img, B, H,
                        W, C, p, gw, N, pad_h / 2, pad_w / 2, P, static_cast<bf16_t*>(out), ldo);
