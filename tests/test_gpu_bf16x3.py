@@ -272,7 +272,8 @@ def _attn_ref64(qkv, B, N, H, dk, dkp):
 
 @pytest.mark.parametrize("B,N,H,dk", [(2, 196, 3, 64), (1, 70, 2, 40), (1, 1, 1, 32),
                                       (1, 333, 2, 128), (2, 1600, 2, 64), (3, 576, 3, 64),
-                                      (40, 196, 12, 64), (1, 64, 4, 20), (1, 129, 2, 100)])
+                                      (40, 196, 12, 64), (1, 64, 4, 20), (1, 129, 2, 100),
+                                      (2, 17, 3, 64), (1, 1, 2, 64), (3, 33, 2, 64)])
 @pytest.mark.parametrize("variant", [-1, 10])
 def test_attention_split_vs_fp64(L, cuda, B, N, H, dk, variant):
     """vtd_attention with dtype VTD_BF16X3 (vtd.py:364-369 in the split-bf16 parity mode): f32
