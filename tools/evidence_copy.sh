@@ -6,6 +6,7 @@ O=gpurun_out/$1; P=profiles/r06_$2
 cp $O/bench.log ${P}_bench.log
 for f in $O/bench_*.log; do cp $f ${P}_$(basename $f); done
 cp $O/gpu_tests.log ${P}_gpu_tests.log
+[ -f $O/smoke.log ] && cp $O/smoke.log ${P}_smoke.log
 cp $O/accuracy.log ${P}_accuracy.log
 cp $O/attn_pmc.json ${P}_attn_pmc.json
 cp $(find $O/prof -name '*kernel_stats.csv' | head -1) ${P}_rocprof_kernel_stats_streams1.csv

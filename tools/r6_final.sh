@@ -11,6 +11,8 @@ mkdir -p $O
 export PYTHONUNBUFFERED=1
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -s --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }
 tail -1 $O/gpu_tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -3 $O/smoke.log
 timeout -k 10 300 python bench.py > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
 tail -1 $O/bench.log | cut -c1-300
 for cfg in "c2_b64_bf16:--batch 64" "c3_b32_bf16:--preset vit_b16_640 --batch 32" \
