@@ -1901,8 +1901,20 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
   }
   ProfScope ps(stream, PROF_GEMM, flops > 0 ? flops : 2.0 * M * N * (double)K);
   const int tiles_m = (M + BBM - 1) / BBM, tiles_n = (N + BBN - 1) / BBN;
-  // N <= 64 (the Dense(17) head projection): 128 x 128 tiles waste 8x less MFMA work
-  if (dtype == VTD_BF16 && tiles_m * tiles_n >= kMinBigTiles && N > 64) {
+  // Kernel choice.  >= kMinBigTiles 256 x 256 tiles: pp2.  Fewer: the skinny kernel for
+  // narrow layers (N <= 320, its Bt image in LDS), else pp2 as well -- a few-tile problem
+  // (small batches: qkv at B = 8 has 63 tiles) runs one round of pp2 tiles at its K loop's
+  // rate, where the 128 x 128 register-staged kernel took 4-8x longer (C2 B = 8: 50 launches
+  // of 87-193 us per forward, profiles/r06_small_batch_pp2_ab.log); VTD_SMALL_PP2=0 restores it.
+  // N <= 64 (the Dense(17) head projection): 128 x 128 tiles waste 8x less MFMA work.
+  static const bool small_pp2 = [] {
+    const char* v = getenv("VTD_SMALL_PP2");
+    return !v || atoi(v) != 0;
+  }();
+  const bool big = tiles_m * tiles_n >= kMinBigTiles && N > 64;
+  const bool skinny = dtype == VTD_BF16 && K - 32 * aw <= SK_KMAX && skinny_choice(M, N, K);
+  const bool few = small_pp2 && N > 64 && !skinny;
+  if (dtype == VTD_BF16 && (big || few)) {
     const bf16_t* a16 = static_cast<const bf16_t*>(A);
     const bf16_t* b16 = static_cast<const bf16_t*>(Bt);
     const int ngw = tile_group_width(tiles_n);
@@ -1992,11 +2004,12 @@ int gemm_launch_ln(int M, int N, int K, const void* A, int lda, const void* Bt, 
       default:
         pp2_launch<EPI_GENERIC>(tr, g, stream, M, N, K, a16, lda, b16, ldb, tiles_m, tiles_n, e);
     }
-  } else if (dtype == VTD_F32 && tiles_m * tiles_n >= kMinBigTiles && N > 64 &&
-             knob(VTD_KNOB_F32_PP2) != 0) {
+  } else if (dtype == VTD_F32 && big && knob(VTD_KNOB_F32_PP2) != 0) {
+    // (f32: few-tile problems stay on the 128 x 128 kernel -- the f32 256-tile kernel measured
+    // 1.7x slower there, C2 B = 8 f32 557 -> 328 img/s)
     f32_pp2_launch(M, N, K, static_cast<const float*>(A), lda, static_cast<const float*>(Bt), ldb,
                    epi, tiles_m, tiles_n, stream);
-  } else if (dtype == VTD_BF16 && K - 32 * aw <= SK_KMAX && skinny_choice(M, N, K)) {
+  } else if (skinny) {
     EpiArgs e = make_epi_args(epi);
     e.aw = aw;
     const dim3 grid((M + SK_ROWS - 1) / SK_ROWS, (N + 31) / 32);
