@@ -251,6 +251,31 @@ bool split_pad() {
 // parts' head launches co-run: +0.2 % at C2 B = 256, +0.9 % at B = 64,
 // profiles/r05_splitk_target_ab.log)
 int splitk_target(int nparts) { return 256 / std::max(nparts, 1); }
+// Split-K count of an encoder Dense layer (M x N, K-steps of 64): the count minimising a model
+// of its time -- rounds of the part's 256 / nparts workgroups x K-steps per split x ~1.5 us,
+// plus the fp32 partials written and read at ~4 TB/s -- if it saves >= 10 % over no split.
+// Few-tile, long-K layers of small batches split (C2 B = 8: mlp2 42 tiles x 48 K-steps);
+// a layer that already fills a round does not (C2 B = 32: splitting mlp2 / mlp3 cost 6 %,
+// profiles/r06_enc_splitk_ab.log).  1 = no split.
+int enc_splitk_choice(int64_t M, int N, int K, int nparts, int dtype) {
+  if ((dtype != VTD_BF16 && dtype != VTD_BF16X3) || M <= 0 || N <= 64 || N % 4 != 0 || K % 64 != 0 || knob(VTD_KNOB_SPLITK) == 0) return 1;
+  const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  const int nk = K / 64, cus = 256 / std::max(nparts, 1);
+  auto rounds = [&](int64_t wgs) { return (double)((wgs + cus - 1) / cus); };
+  const double t1 = rounds(tiles) * nk * 1.5;
+  double best = 0.9 * t1;
+  int bs = 1;
+  for (int sp = 2; sp <= std::min(16, nk / 4); ++sp) {
+    const int nks = (nk + sp - 1) / sp;
+    if ((sp - 1) * nks >= nk) continue;                   // every split non-empty
+    const double t = rounds(tiles * sp) * nks * 1.5 + 2.0 * sp * (double)M * N * 4 / 4e6;
+    if (t < best) {
+      best = t;
+      bs = sp;
+    }
+  }
+  return bs;
+}
 Plan make_plan(const vtd_config* c, const vtd_dims& d, int nparts = 1) {
   const bool pad = nparts > 1 && split_pad();
   Plan p{};
@@ -288,6 +313,16 @@ Plan make_plan(const vtd_config* c, const vtd_dims& d, int nparts = 1) {
                                      c->dtype == VTD_BF16X3 ? VTD_BF16X3 : act_dtype(c->dtype),
                                      splitk_target(nparts));
     if (s > 1) sk = std::max(sk, (size_t)s * HR * d.head_units_p[j] * 4);
+  }
+  // and of the encoder's few-tile Dense layers (small batches, enc_gemm; not VTD_FP8)
+  if (c->dtype != VTD_FP8) {
+    auto enc = [&](int n, int k) {
+      const int s = enc_splitk_choice((int64_t)R, n, opk(c->dtype, k), nparts, c->dtype);
+      if (s > 1) sk = std::max(sk, (size_t)s * R * n * 4);
+    };
+    enc(d.qkv_p, d.d_p);
+    enc(d.d_p, d.inner_p);
+    for (int j = 0, k = d.d_p; j < c->mlp_quantities; k = d.mlp_units_p[j], ++j) enc(d.mlp_units_p[j], k);
   }
   p.splitk = take(sk);
   // VTD_FP8: one MX-fp8 copy of the current encoder GEMM's A operand + its scales
@@ -603,7 +638,20 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
   // against the MX-fp8 weights (W [Np][K8], S [K8/128][Np][4])
   auto enc_gemm = [&](int Np, int K, const void* a, const void* W, const uint8_t* S,
                       const vtd_epilogue* e, double flops) -> int {
-    if (!fp8) return gemm_launch(M, Np, kk(K), a, ka(K), W, kk(K), gdt, e, st, flops);
+    if (!fp8) {
+      // few-tile, long-K layers (small batches) split K (enc_splitk_choice);
+      // not with the LayerNorm fold or partial statistics, which the split-K epilogue lacks
+      static const bool enc_split = [] {      // VTD_ENC_SPLITK=0: off (A/B)
+        const char* v = getenv("VTD_ENC_SPLITK");
+        return !v || atoi(v) != 0;
+      }();
+      const int ks = !enc_split || e->statout || e->lnstat
+                         ? 1 : enc_splitk_choice(M, Np, kk(K), nparts, gdt);
+      if (ks > 1)
+        return gemm_splitk_launch(M, Np, kk(K), a, ka(K), W, kk(K), gdt, e,
+                                  reinterpret_cast<float*>(ws + P.splitk), ks, st, flops);
+      return gemm_launch(M, Np, kk(K), a, ka(K), W, kk(K), gdt, e, st, flops);
+    }
     const int K8 = k8_of(K);
     int r = quantize_mx8_launch(a, VTD_BF16, R, K, K, K8, q8, K8, s8, P.s8_rows, st);
     if (r) return r;
