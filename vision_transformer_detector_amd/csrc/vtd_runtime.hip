@@ -203,7 +203,7 @@ static int derive(const vtd_config* c, vtd_dims* d) {
 namespace {
 struct Plan {
   size_t patches, x, xb, h, stat, pstat, qkv, attn, attn3, mlp0, mlp1, u, head0, head1, q8, s8, q8b,
-      s8b, splitk, total;
+      s8b, splitk, splitk_bytes, total;
   int k8_max;                       // widest MX-fp8 GEMM K (VTD_FP8)
   int64_t s8_rows;                  // activation scale rows (rows rounded up to 4)
 };
@@ -256,8 +256,11 @@ int splitk_target(int nparts) { return 256 / std::max(nparts, 1); }
 // plus the fp32 partials written and read at ~4 TB/s -- if it saves >= 10 % over no split.
 // Few-tile, long-K layers of small batches split (C2 B = 8: mlp2 42 tiles x 48 K-steps);
 // a layer that already fills a round does not (C2 B = 32: splitting mlp2 / mlp3 cost 6 %,
-// profiles/r06_enc_splitk_ab.log).  1 = no split.
-int enc_splitk_choice(int64_t M, int N, int K, int nparts, int dtype) {
+// profiles/r06_enc_splitk_ab.log).  Only counts whose partials fit max_bytes (the plan's
+// kEncSplitBytes: a batch-independent reserve, so the workspace stays monotonic in the batch).
+// 1 = no split.
+constexpr size_t kEncSplitBytes = size_t(64) << 20;
+int enc_splitk_choice(int64_t M, int N, int K, int nparts, int dtype, size_t max_bytes) {
   if ((dtype != VTD_BF16 && dtype != VTD_BF16X3) || M <= 0 || N <= 64 || N % 4 != 0 || K % 64 != 0 || knob(VTD_KNOB_SPLITK) == 0) return 1;
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
   const int nk = K / 64, cus = 256 / std::max(nparts, 1);
@@ -268,6 +271,7 @@ int enc_splitk_choice(int64_t M, int N, int K, int nparts, int dtype) {
   for (int sp = 2; sp <= std::min(16, nk / 4); ++sp) {
     const int nks = (nk + sp - 1) / sp;
     if ((sp - 1) * nks >= nk) continue;                   // every split non-empty
+    if ((size_t)sp * M * N * 4 > max_bytes) break;
     const double t = rounds(tiles * sp) * nks * 1.5 + 2.0 * sp * (double)M * N * 4 / 4e6;
     if (t < best) {
       best = t;
@@ -314,16 +318,10 @@ Plan make_plan(const vtd_config* c, const vtd_dims& d, int nparts = 1) {
                                      splitk_target(nparts));
     if (s > 1) sk = std::max(sk, (size_t)s * HR * d.head_units_p[j] * 4);
   }
-  // and of the encoder's few-tile Dense layers (small batches, enc_gemm; not VTD_FP8)
-  if (c->dtype != VTD_FP8) {
-    auto enc = [&](int n, int k) {
-      const int s = enc_splitk_choice((int64_t)R, n, opk(c->dtype, k), nparts, c->dtype);
-      if (s > 1) sk = std::max(sk, (size_t)s * R * n * 4);
-    };
-    enc(d.qkv_p, d.d_p);
-    enc(d.d_p, d.inner_p);
-    for (int j = 0, k = d.d_p; j < c->mlp_quantities; k = d.mlp_units_p[j], ++j) enc(d.mlp_units_p[j], k);
-  }
+  // and of the encoder's few-tile Dense layers (small batches, enc_gemm; bf16 operands): a
+  // fixed reserve, whose size bounds their split counts (enc_splitk_choice)
+  if (c->dtype == VTD_BF16 || c->dtype == VTD_BF16X3) sk = std::max(sk, kEncSplitBytes);
+  p.splitk_bytes = sk;
   p.splitk = take(sk);
   // VTD_FP8: one MX-fp8 copy of the current encoder GEMM's A operand + its scales
   p.k8_max = 0;
@@ -646,7 +644,7 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
         return !v || atoi(v) != 0;
       }();
       const int ks = !enc_split || e->statout || e->lnstat
-                         ? 1 : enc_splitk_choice(M, Np, kk(K), nparts, gdt);
+                         ? 1 : enc_splitk_choice(M, Np, kk(K), nparts, gdt, P.splitk_bytes);
       if (ks > 1)
         return gemm_splitk_launch(M, Np, kk(K), a, ka(K), W, kk(K), gdt, e,
                                   reinterpret_cast<float*>(ws + P.splitk), ks, st, flops);
