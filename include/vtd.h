@@ -231,7 +231,7 @@ int vtd_gemm(int M, int N, int K, const void* A_dev, int lda, const void* Bt_dev
  * K / 64 / ksplit
  * K-steps each write fp32 partial sums into part_dev ([ksplit][M][N] floats,
  * part_bytes >= ksplit * M * N * 4), then one pass sums them in split order and applies
- * the epilogue (no LayerNorm fold / statistics).  K % 64 == 0, N % 4 == 0,
+ * the epilogue (the LayerNorm fold included; no partial statistics).  K % 64 == 0, N % 4 == 0,
  * 2 <= ksplit <= K / 64 with every split non-empty.  vtd_gemm_splitk_choice returns the
  * split count vtd_forward uses for (M, N, K, dtype) (1 = no split). */
 int vtd_gemm_splitk(int M, int N, int K, const void* A_dev, int lda, const void* Bt_dev,

@@ -950,3 +950,36 @@ def test_gemm_tiles_per_workgroup(L, cuda, M, N, K, act, mode, tpw):
     assert torch.equal(x1, x2)
     if s1 is not None:
         assert torch.equal(s1, s2)
+
+
+@pytest.mark.parametrize("M,N,K,ks", [(1568, 2304, 768, 3), (196, 3072, 768, 6)])
+def test_gemm_splitk_layernorm_fold(L, cuda, M, N, K, ks):
+    """vtd_gemm_splitk with the LayerNorm fold (epilogue.lnstat / colsum, applied in the
+    reduction's epilogue: what vtd_forward's small-batch query/key/value and first MLP layers
+    run) against the unsplit kernel on the same operands: equal up to fp32 summation order."""
+    g = torch.Generator(device=cuda).manual_seed(M + N + ks)
+    A = torch.randn(M, K, generator=g, device=cuda).to(torch.bfloat16)
+    Bt = (torch.randn(N, K, generator=g, device=cuda) / math.sqrt(K)).to(torch.bfloat16)
+    bias = torch.randn(N, generator=g, device=cuda)
+    mean = torch.randn(M, generator=g, device=cuda) * 0.1
+    rstd = torch.rand(M, generator=g, device=cuda) + 0.5
+    lnstat = torch.stack([mean, rstd], 1).contiguous()
+    colsum = Bt.float().sum(1).contiguous()
+    outs = []
+    for split in (1, ks):
+        out = torch.full((M, N), float("nan"), device=cuda)
+        e = L.VtdEpilogue()
+        e.bias, e.act, e.out, e.ldo, e.out_dtype = L.ptr(bias), 1, L.ptr(out), N, 0
+        e.lnstat, e.colsum = lnstat.data_ptr(), colsum.data_ptr()
+        if split == 1:
+            L.check(L.lib.vtd_gemm(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, L.BF16,
+                                   ctypes.byref(e), L.stream_ptr()), "vtd_gemm")
+        else:
+            part = torch.empty(split * M * N, device=cuda)
+            L.check(L.lib.vtd_gemm_splitk(M, N, K, A.data_ptr(), K, Bt.data_ptr(), K, L.BF16,
+                                          ctypes.byref(e), part.data_ptr(), part.numel() * 4,
+                                          split, L.stream_ptr()), "vtd_gemm_splitk")
+        outs.append(out)
+    torch.cuda.synchronize()
+    d = (outs[0].double() - outs[1].double()).abs().max().item()
+    assert d <= 1e-5 * max(1.0, outs[0].abs().max().item()), d

@@ -2084,8 +2084,11 @@ int gemm_splitk_launch(int M, int N, int K, const void* A, int lda, const void* 
   VTD_CHECK_ARG((split_a || lda >= K) && ldb >= K && lda % 8 == 0 && ldb % 8 == 0,
                 "gemm_splitk: lda/ldb must be >= K and multiples of 8");
   VTD_CHECK_ARG(ksplit >= 2 && ksplit <= K / 64, "gemm_splitk: ksplit");
-  VTD_CHECK_ARG(!epi->statout && !epi->lnstat,
-                "gemm_splitk: LayerNorm statistics / fold are not supported");
+  // (the LayerNorm fold applies in the reduction's epilogue; partial statistics are not written)
+  VTD_CHECK_ARG(!epi->statout, "gemm_splitk: LayerNorm partial statistics are not supported");
+  VTD_CHECK_ARG(!epi->lnstat || (epi->colsum && reinterpret_cast<uintptr_t>(epi->lnstat) % 8 == 0 &&
+                                 reinterpret_cast<uintptr_t>(epi->colsum) % 16 == 0),
+                "gemm_splitk: lnstat needs colsum (16-B aligned) and 8-B alignment");
   const int nk = K / 64, nks = (nk + ksplit - 1) / ksplit;
   VTD_CHECK_ARG((ksplit - 1) * nks < nk, "gemm_splitk: an empty split");
   ProfScope ps(stream, PROF_GEMM, flops > 0 ? flops : 2.0 * M * N * (double)K);

@@ -638,12 +638,12 @@ int forward_impl(const vtd_config* cfg, const vtd_weights* w, const float* image
                       const vtd_epilogue* e, double flops) -> int {
     if (!fp8) {
       // few-tile, long-K layers (small batches) split K (enc_splitk_choice);
-      // not with the LayerNorm fold or partial statistics, which the split-K epilogue lacks
+      // not with partial statistics, which the split-K epilogue does not write
       static const bool enc_split = [] {      // VTD_ENC_SPLITK=0: off (A/B)
         const char* v = getenv("VTD_ENC_SPLITK");
         return !v || atoi(v) != 0;
       }();
-      const int ks = !enc_split || e->statout || e->lnstat
+      const int ks = !enc_split || e->statout
                          ? 1 : enc_splitk_choice(M, Np, kk(K), nparts, gdt, P.splitk_bytes);
       if (ks > 1)
         return gemm_splitk_launch(M, Np, kk(K), a, ka(K), W, kk(K), gdt, e,
