@@ -450,8 +450,9 @@ int vtd_profile_read(double* ms, int64_t* launches, double* flops, int n_classes
  *     1 = the register-staged first kernel.
  *   VTD_KNOB_ATTN_GRID (VTD_ATTN_GRID): persistent attention workgroups (default: CUs).
  *   VTD_KNOB_GEMM_NGW (VTD_GEMM_NGW): GEMM tile-order group width (0 = row-major).
- *   VTD_KNOB_SPLITK (VTD_SPLITK): 0 disables the head's split-K, a value >= 64 sets its
- *     workgroup target per launch (default 256); both change the workspace size.
+ *   VTD_KNOB_SPLITK (VTD_SPLITK): 0 disables split-K (the head's and, at small batches, the
+ *     encoder's), a value >= 64 sets the head's workgroup target per launch (default 256);
+ *     both change the workspace size.
  *   VTD_KNOB_JPEG_CHUNK_BITS (VTD_JPEG_CHUNK_BITS): Huffman chunk length of vtd_jpeg_decode.
  *   VTD_KNOB_SKINNY (VTD_SKINNY): 0 keeps the head's narrow bf16 layers (N <= 320) on the
  *     128 x 128 kernel instead of the skinny one; a value >= 64 sets the N threshold (such
